@@ -1,0 +1,58 @@
+"""Build libaiyagari.so (hand-written HIP for gfx950) in-tree.
+
+``python -m aiyagari_hark_amd.build`` compiles ``csrc/*.hip`` with hipcc into
+``aiyagari_hark_amd/lib/libaiyagari.so``.  The shared object is git-ignored but
+travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libaiyagari.so")
+SOURCES = ["api.hip", "egm.hip", "panel.hip", "hist.hip"]
+HEADERS = ["common.h", "internal.h"]
+ARCH = os.environ.get("AIY_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found; the MI355X build needs ROCm's hipcc")
+
+
+def needs_rebuild() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(HERE, "..", "include", "aiyagari.h"))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_rebuild():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
+           "-I/opt/rocm/include"]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    cmd += ["-L/opt/rocm/lib", "-lrccl", "-o", tmp]
+    if verbose:
+        print("[aiyagari build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB)

@@ -1,0 +1,89 @@
+// Handle lifecycle, errors and the RCCL binding of libaiyagari.
+#include "internal.h"
+
+#include <cstring>
+#include <new>
+
+extern "C" int32_t aiy_version(void) { return 100; }  // 0.1.0
+
+extern "C" int32_t aiy_create(int32_t device, aiy_handle** out) {
+  if (!out) return AIY_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return AIY_ERR_HIP;
+  if (device < 0 || device >= n) return AIY_ERR_ARG;
+  aiy_handle* h = new (std::nothrow) aiy_handle();
+  if (!h) return AIY_ERR_STATE;
+  h->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete h;
+    return AIY_ERR_HIP;
+  }
+  *out = h;
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_destroy(aiy_handle* h) {
+  if (!h) return AIY_OK;
+  (void)hipSetDevice(h->device);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->d_dist) (void)hipFree(h->d_dist);
+  if (h->d_last) (void)hipFree(h->d_last);
+  if (h->h_dist) (void)hipHostFree(h->h_dist);
+  if (h->h_last) (void)hipHostFree(h->h_last);
+  if (h->d_partials) (void)hipFree(h->d_partials);
+  if (h->d_hdist) (void)hipFree(h->d_hdist);
+  if (h->d_K) (void)hipFree(h->d_K);
+  if (h->d_hlast) (void)hipFree(h->d_hlast);
+  if (h->h_hdist) (void)hipHostFree(h->h_hdist);
+  if (h->h_K) (void)hipHostFree(h->h_K);
+  if (h->h_hlast) (void)hipHostFree(h->h_hlast);
+  delete h;
+  return AIY_OK;
+}
+
+extern "C" const char* aiy_last_error(const aiy_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+extern "C" int32_t aiy_comm_unique_id(void* out128) {
+  if (!out128) return AIY_ERR_ARG;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return AIY_ERR_COMM;
+  std::memcpy(out128, &id, sizeof(id));
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_comm_init(aiy_handle* h, const void* unique_id128, int32_t nranks, int32_t rank) {
+  if (!h) return AIY_ERR_ARG;
+  if (!unique_id128 || nranks < 1 || rank < 0 || rank >= nranks) return aiy::fail(h, AIY_ERR_ARG, "bad comm args");
+  if (h->comm) return aiy::fail(h, AIY_ERR_STATE, "communicator already bound");
+  AIY_HIP(h, hipSetDevice(h->device));
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id128, sizeof(id));
+  ncclResult_t r = ncclCommInitRank(&h->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    h->comm = nullptr;
+    return aiy::fail(h, AIY_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  h->nranks = nranks;
+  h->rank = rank;
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_comm_destroy(aiy_handle* h) {
+  if (!h) return AIY_ERR_ARG;
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  h->comm = nullptr;
+  h->nranks = 1;
+  h->rank = 0;
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_allreduce_sum(aiy_handle* h, double* buf, int64_t n, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (!h->comm) return aiy::fail(h, AIY_ERR_STATE, "no communicator bound");
+  if (!buf || n < 0) return aiy::fail(h, AIY_ERR_ARG, "bad buffer");
+  ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, h->comm, aiy::as_stream(stream));
+  if (r != ncclSuccess) return aiy::fail(h, AIY_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+  return AIY_OK;
+}

@@ -1,0 +1,166 @@
+// Shared device helpers for libaiyagari (gfx950 / CDNA4, wave64).
+//
+// Numerics policy: the library is compiled with -ffp-contract=off so every product and
+// sum rounds exactly as the NumPy expressions of the reference do
+// (Aiyagari_Support.py:1024, 1485, 1490, 1499; HARK LinearInterp /
+// LinearInterpOnInterp1D).  Sums over next-period states replicate NumPy's pairwise
+// summation order (8 running partials, numpy/_core/src/umath/loops_utils.h) so the
+// CRRA = 1 path is bit-identical to the oracle; other CRRA values differ only by the
+// device pow's last-ulp rounding.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace aiy {
+
+constexpr int kWave = 64;
+constexpr double kBorrowNode = 0.0000001;  // Aiyagari_Support.py:1503-1504
+
+// ---------------------------------------------------------------------------------
+// Wave-level helpers
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+// NaN-propagating max (np.max semantics): a NaN anywhere makes the result NaN.
+__device__ __forceinline__ double nan_max(double a, double b) {
+  return (a != a || a > b) ? a : b;
+}
+__device__ __forceinline__ double wave_nan_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------
+// Lower bound (numpy searchsorted side='left') over x[lo, hi): first index with
+// x[idx] >= q, or hi.  For a sorted row every correct lower bound returns the index
+// numpy's npy_binsearch<left> returns.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ int lower_bound(const double* __restrict__ x, int lo, int hi, double q) {
+  while (lo < hi) {
+    int mid = lo + ((hi - lo) >> 1);
+    if (x[mid] < q) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// HARK 0.12 LinearInterp._evaluate for one query given the bracket index
+// i = max(searchsorted(x[:-1], q), 1):
+//   alpha = (q - x[i-1]) / (x[i] - x[i-1]); y = (1 - alpha) y[i-1] + alpha y[i];
+//   NaN when q < x[0] (lower_extrap = False).
+__device__ __forceinline__ double lerp_at(const double* __restrict__ x, const double* __restrict__ y,
+                                          int i, double q, double x0) {
+  double xl = x[i - 1], xh = x[i];
+  double alpha = (q - xl) / (xh - xl);
+  double v = (1.0 - alpha) * y[i - 1] + alpha * y[i];
+  return (q < x0) ? __builtin_nan("") : v;
+}
+
+// Wave-cooperative monotone interpolation on one row (x, y) of length n + 1.
+// All 64 lanes of the wave must call it together (inactive lanes pass active=false).
+// The bracket search is narrowed to [lb(qmin), lb(qmax)] found by two wave-uniform
+// searches, so each lane's private search runs over a few dozen nodes instead of n.
+__device__ __forceinline__ double interp_row_wave(const double* __restrict__ x, const double* __restrict__ y,
+                                                  int n, double q, bool active) {
+  double qmin = wave_min(active ? q : __builtin_inf());
+  double qmax = wave_max(active ? q : -__builtin_inf());
+  int lo = 0, hi = n;
+  if (qmin == qmin && qmax == qmax && qmin <= qmax) {   // all-NaN / no active lanes: full search
+    lo = lower_bound(x, 0, n, qmin);
+    hi = lower_bound(x, lo, n, qmax);   // lb(q) lies in [lb(qmin), lb(qmax)] for q in range
+  }
+  int i = lower_bound(x, lo, hi, q);    // NaN lanes get some index; their value is NaN anyway
+  i = i < 1 ? 1 : i;
+  return lerp_at(x, y, i, q, x[0]);
+}
+
+// Plain per-lane search version (no wave cooperation); used where lanes are independent.
+__device__ __forceinline__ double interp_row(const double* __restrict__ x, const double* __restrict__ y,
+                                             int n, double q) {
+  int i = lower_bound(x, 0, n, q);
+  i = i < 1 ? 1 : i;
+  return lerp_at(x, y, i, q, x[0]);
+}
+
+// ---------------------------------------------------------------------------------
+// x ** -gam and x ** (-1/gam) with NumPy's fast scalar-power path for gam == 1
+// (ndarray ** -1.0 is np.reciprocal).  kind: 1 -> gam == 1; 0 -> generic pow.
+// ---------------------------------------------------------------------------------
+template <int KIND>
+__device__ __forceinline__ double crra_marg(double c, double gam) {
+  if constexpr (KIND == 1) return 1.0 / c;
+  else return pow(c, -gam);
+}
+template <int KIND>
+__device__ __forceinline__ double crra_inv(double e, double gam) {
+  if constexpr (KIND == 1) return 1.0 / e;
+  else return pow(e, -1.0 / gam);
+}
+
+// ---------------------------------------------------------------------------------
+// NumPy pairwise sum of f(0..n) for n <= NMAX <= 128 (numpy's pairwise_sum for
+// n <= PW_BLOCKSIZE): n < 8 -> sequential from 0.0; else 8 running partials r[t % 8]
+// over t < n - n % 8, combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail added
+// in order.  Every f(t) index is a compile-time constant so register arrays behind f
+// stay in registers.
+// ---------------------------------------------------------------------------------
+template <int NMAX, typename F>
+__device__ __forceinline__ double np_pairwise_sum(int n, F f) {
+  if (n < 8) {
+    double res = 0.0;
+#pragma unroll
+    for (int t = 0; t < (NMAX < 8 ? NMAX : 8); ++t)
+      if (t < n) res += f(t);
+    return res;
+  }
+  if constexpr (NMAX >= 8) {
+    const int nfull = n - (n % 8);
+    double r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) r[t] = f(t);
+#pragma unroll
+    for (int t = 8; t < NMAX; ++t)
+      if (t < nfull) r[t % 8] += f(t);
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int t = 8; t < NMAX; ++t)
+      if (t >= nfull && t < n) res += f(t);
+    return res;
+  } else {
+    return 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Philox4x32-10 (Random123 constants) and the 53-bit uniform used by the panel.
+// counter = (c0, idx_lo, idx_hi, stream), key = (seed_lo, seed_hi).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ double philox_uniform(uint32_t ctr0, uint64_t idx, uint64_t seed, uint32_t stream) {
+  uint32_t c[4] = {ctr0, (uint32_t)idx, (uint32_t)(idx >> 32), stream};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  double a = (double)(c[0] >> 5), b = (double)(c[1] >> 6);
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+}  // namespace aiy

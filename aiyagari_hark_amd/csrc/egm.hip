@@ -1,0 +1,325 @@
+// EGM backward step for gfx950.
+//
+// One launch == one call of solve_Aiyagari (Aiyagari_Support.py:1423-1520) for every
+// calibration of a batch.  Work decomposition (MI355X-first, not a translation of the
+// reference's 4-D NumPy tiling):
+//   * the reference tiles mNext/Mnext/R/P to [a, M, s, s'] (precompute_arrays,
+//     Aiyagari_Support.py:906-1037) and evaluates every next-period marginal value 28x
+//     (once per current state s).  Here a thread owns one (calibration, M node k,
+//     asset node i) and evaluates V[s'] = R[k,s'] * c_{s'}(m'(i,k,s'), M'[k,s'])^-rho
+//     ONCE per s', keeping all S values in registers;
+//   * the expectation E[s] = beta * sum_{s'} V[s'] P[s,s'] (AS:1485) is then an S x S
+//     register contraction per thread, summed in NumPy's pairwise order, with P read
+//     through the scalar cache (block-uniform addresses);
+//   * next-period consumption c_{s'}(m, M') is HARK's LinearInterpOnInterp1D over the
+//     two M rows that bracket M' (block-uniform), each a LinearInterp whose bracket is
+//     found by a wave-cooperative monotone search: queries m'(i) = R a_i + W l are
+//     increasing in i, so the wave finds [lb(q_min), lb(q_max)] with two wave-uniform
+//     searches and each lane searches only that window;
+//   * outputs (m, c) are written row-contiguous in i (coalesced), node 0 is the
+//     (1e-7, 1e-7) point (AS:1503-1504), and in solve mode the HARK distance
+//     (max |dm|, |dc|) is reduced per block and folded into a per-calibration slot
+//     with a 64-bit atomicMax on the bit pattern of the non-negative double.
+#include "common.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace aiy {
+
+constexpr int kEgmBlock = 128;
+
+struct EgmDev {
+  int n_cal, S, n_M, n_a;
+  const double* a_grid;
+  const double* M_grid;
+  const double* P;
+  const double* R_next;
+  const double* W_next;
+  const double* M_next;
+  const double* lab;
+  const double* beta;
+  const double* crra;
+};
+
+// Convergence protocol (solve mode, dist_slots != nullptr): cycle n reads slot
+// (n-1)%3 and returns at once if cycle n-1 already met !(d > tol) (HARK:
+// go = distance > tolerance), folds its own distance into slot n%3, and zeroes
+// slot (n+1)%3 for cycle n+1.  A skipped cycle writes nothing, so every later cycle
+// also sees a zero slot and skips: convergence is sticky without host involvement.
+template <int SMAX, bool TERMINAL>
+__global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const double* __restrict__ m_next,
+                                                              const double* __restrict__ c_next,
+                                                              double* __restrict__ m_out,
+                                                              double* __restrict__ c_out, int cycle,
+                                                              unsigned long long* dist_slots,
+                                                              int* last_cycle, double tol) {
+  const int cal = blockIdx.z;
+  const int k = blockIdx.y;
+  if (dist_slots != nullptr && cycle >= 3) {
+    const double dprev = __longlong_as_double((long long)dist_slots[cal * 3 + (cycle - 1) % 3]);
+    if (!(dprev > tol)) return;
+  }
+  const int S = A.S, n_M = A.n_M, n_a = A.n_a, n1 = n_a + 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n_a;
+  const double a = A.a_grid[(size_t)cal * n_a + (active ? i : n_a - 1)];
+  const double gam = A.crra[cal];
+  const double beta = A.beta[cal];
+  const bool log_util = (gam == 1.0);  // NumPy fast path: x ** -1.0 is np.reciprocal
+  const double* Rk = A.R_next + ((size_t)cal * n_M + k) * S;
+  const double* Wk = A.W_next + ((size_t)cal * n_M + k) * S;
+  const double* Mk = A.M_next + ((size_t)cal * n_M + k) * S;
+  const double* lab = A.lab + (size_t)cal * S;
+  const double* Mg = A.M_grid + (size_t)cal * n_M;
+  const size_t tab_cal = (size_t)cal * S * n_M * n1;
+
+  // Phase 1 (runtime loop over s'): V[s'] = R * vP_{s'}(m', M') staged in LDS, one
+  // column per lane (conflict-free), so the unrolled contraction below can pull the
+  // whole vector into registers with compile-time indices.
+  __shared__ double Vs[SMAX * kEgmBlock];
+  for (int sp = 0; sp < S; ++sp) {
+    const double R = Rk[sp];
+    const double q = R * a + Wk[sp] * lab[sp];  // mNextArray (AS:1024)
+    double c;
+    if constexpr (TERMINAL) {
+      c = q * 1.0;  // IdentityFunction (AS:898)
+    } else {
+      const double* bm = m_next + tab_cal + (size_t)sp * n_M * n1;
+      const double* bc = c_next + tab_cal + (size_t)sp * n_M * n1;
+      if (n_M == 1) {
+        c = interp_row_wave(bm, bc, n_a, q, active);
+      } else {
+        // LinearInterpOnInterp1D: y_pos = clip(searchsorted(Mgrid, M'), 1, n_M - 1)
+        const double Mp = Mk[sp];
+        int j = lower_bound(Mg, 0, n_M, Mp);
+        j = j > n_M - 1 ? n_M - 1 : j;
+        j = j < 1 ? 1 : j;
+        const double alpha = (Mp - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
+        const double f0 = interp_row_wave(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, n_a, q, active);
+        const double f1 = interp_row_wave(bm + (size_t)j * n1, bc + (size_t)j * n1, n_a, q, active);
+        c = (1 - alpha) * f0 + alpha * f1;
+      }
+    }
+    const double vP = log_util ? 1.0 / c : pow(c, -gam);  // MargValueFuncCRRA
+    Vs[sp * kEgmBlock + threadIdx.x] = R * vP;             // RnextArray * vPnext
+  }
+  double V[SMAX];
+#pragma unroll
+  for (int sp = 0; sp < SMAX; ++sp) V[sp] = (sp < S) ? Vs[sp * kEgmBlock + threadIdx.x] : 0.0;
+
+  const double* Pc = A.P + (size_t)cal * S * S;
+  double dmax = 0.0;
+  const bool track = (dist_slots != nullptr) && cycle >= 2;
+  for (int s = 0; s < S; ++s) {
+    const double* Ps = Pc + (size_t)s * S;
+    const double sum = np_pairwise_sum<SMAX>(S, [&](int t) { return V[t] * Ps[t]; });
+    const double E = beta * sum;                                   // EndOfPrdvP (AS:1485)
+    const double c = log_util ? 1.0 / E : pow(E, -1.0 / gam);      // AS:1490
+    const double m = a + c;                                        // AS:1499
+    const size_t row = tab_cal + ((size_t)s * n_M + k) * n1;
+    if (active) {
+      m_out[row + i + 1] = m;
+      c_out[row + i + 1] = c;
+      if (track) dmax = nan_max(dmax, nan_max(fabs(m - m_next[row + i + 1]), fabs(c - c_next[row + i + 1])));
+    }
+    if (i == 0) {
+      m_out[row] = kBorrowNode;
+      c_out[row] = kBorrowNode;
+    }
+  }
+
+  if (dist_slots != nullptr) {
+    if (track) {
+      __shared__ double red[kEgmBlock / kWave];
+      dmax = wave_nan_max(dmax);
+      if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = dmax;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double d = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) d = nan_max(d, red[w]);
+        atomicMax(&dist_slots[cal * 3 + cycle % 3], (unsigned long long)__double_as_longlong(d));
+      }
+    }
+    if (blockIdx.x == 0 && k == 0 && threadIdx.x == 0) {
+      dist_slots[cal * 3 + (cycle + 1) % 3] = 0ull;
+      last_cycle[cal] = cycle;
+    }
+  }
+}
+
+// cFunc[state](m, M) for arbitrary queries (HARK LinearInterpOnInterp1D scalar-M path).
+__global__ void policy_eval_kernel(int S, int n_M, int n_a, const double* __restrict__ m_tab,
+                                   const double* __restrict__ c_tab, const double* __restrict__ Mg,
+                                   const int* __restrict__ state, const double* __restrict__ mq,
+                                   const double* __restrict__ Mq, long long n, double* __restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int s = state[t];
+  const int n1 = n_a + 1;
+  const double q = mq[t];
+  if (s < 0 || s >= S) { out[t] = __builtin_nan(""); return; }
+  const double* bm = m_tab + (size_t)s * n_M * n1;
+  const double* bc = c_tab + (size_t)s * n_M * n1;
+  if (n_M == 1) { out[t] = interp_row(bm, bc, n_a, q); return; }
+  const double M = Mq[t];
+  int j = lower_bound(Mg, 0, n_M, M);
+  j = j > n_M - 1 ? n_M - 1 : j;
+  j = j < 1 ? 1 : j;
+  const double alpha = (M - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
+  const double f0 = interp_row(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, n_a, q);
+  const double f1 = interp_row(bm + (size_t)j * n1, bc + (size_t)j * n1, n_a, q);
+  out[t] = (1 - alpha) * f0 + alpha * f1;
+}
+
+static int32_t check_egm(aiy_handle* h, const aiy_egm_dims* d, const aiy_egm_inputs* in) {
+  if (!h) return AIY_ERR_ARG;
+  if (!d || !in) return fail(h, AIY_ERR_ARG, "null dims/inputs");
+  if (d->n_cal < 1 || d->S < 1 || d->n_M < 1 || d->n_a < 2)
+    return fail(h, AIY_ERR_ARG, "bad dims n_cal=%d S=%d n_M=%d n_a=%d", d->n_cal, d->S, d->n_M, d->n_a);
+  if (d->S > AIY_MAX_STATES) return fail(h, AIY_ERR_UNSUPPORTED, "S=%d exceeds %d", d->S, AIY_MAX_STATES);
+  if (d->n_cal > 65535 || d->n_M > 65535) return fail(h, AIY_ERR_UNSUPPORTED, "grid too large");
+  if (!in->a_grid || !in->P || !in->R_next || !in->W_next || !in->lab || !in->beta || !in->crra)
+    return fail(h, AIY_ERR_ARG, "null input array");
+  if (d->n_M > 1 && (!in->M_grid || !in->M_next)) return fail(h, AIY_ERR_ARG, "null M_grid/M_next");
+  return AIY_OK;
+}
+
+static EgmDev to_dev(const aiy_egm_dims* d, const aiy_egm_inputs* in) {
+  EgmDev A;
+  A.n_cal = d->n_cal; A.S = d->S; A.n_M = d->n_M; A.n_a = d->n_a;
+  A.a_grid = in->a_grid; A.M_grid = in->M_grid; A.P = in->P; A.R_next = in->R_next;
+  A.W_next = in->W_next; A.M_next = in->M_next; A.lab = in->lab; A.beta = in->beta; A.crra = in->crra;
+  return A;
+}
+
+template <bool TERM>
+static void launch_cycle_t(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co,
+                           int cycle, unsigned long long* ds, int* lc, double tol, hipStream_t st) {
+  dim3 grid((A.n_a + kEgmBlock - 1) / kEgmBlock, A.n_M, A.n_cal);
+  dim3 block(kEgmBlock);
+  if (A.S <= 8)
+    hipLaunchKernelGGL((egm_cycle_kernel<8, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+  else if (A.S <= 16)
+    hipLaunchKernelGGL((egm_cycle_kernel<16, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+  else if (A.S <= 32)
+    hipLaunchKernelGGL((egm_cycle_kernel<32, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+  else
+    hipLaunchKernelGGL((egm_cycle_kernel<64, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+}
+
+static void launch_cycle(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co, int cycle,
+                         unsigned long long* ds, int* lc, double tol, hipStream_t st) {
+  if (mn == nullptr) launch_cycle_t<true>(A, mn, cn, mo, co, cycle, ds, lc, tol, st);
+  else launch_cycle_t<false>(A, mn, cn, mo, co, cycle, ds, lc, tol, st);
+}
+
+static int32_t ensure_egm_scratch(aiy_handle* h, int n_cal) {
+  if ((size_t)n_cal <= h->egm_cap) return AIY_OK;
+  if (h->d_dist) { (void)hipFree(h->d_dist); (void)hipFree(h->d_last); }
+  if (h->h_dist) { (void)hipHostFree(h->h_dist); (void)hipHostFree(h->h_last); }
+  h->d_dist = nullptr; h->d_last = nullptr; h->h_dist = nullptr; h->h_last = nullptr; h->egm_cap = 0;
+  AIY_HIP(h, hipMalloc((void**)&h->d_dist, sizeof(unsigned long long) * 3 * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_last, sizeof(int) * n_cal));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_dist, sizeof(unsigned long long) * 3 * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_last, sizeof(int) * n_cal, hipHostMallocDefault));
+  h->egm_cap = n_cal;
+  return AIY_OK;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
+                                const double* m_next, const double* c_next, double* m_out, double* c_out,
+                                aiy_stream stream) {
+  int32_t rc = check_egm(h, dims, in);
+  if (rc) return rc;
+  if ((m_next == nullptr) != (c_next == nullptr)) return fail(h, AIY_ERR_ARG, "m_next/c_next must both be set or NULL");
+  if (!m_out || !c_out) return fail(h, AIY_ERR_ARG, "null output");
+  AIY_HIP(h, hipSetDevice(h->device));
+  EgmDev A = to_dev(dims, in);
+  launch_cycle(A, m_next, c_next, m_out, c_out, 0, nullptr, nullptr, 0.0, as_stream(stream));
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                                 int32_t max_cycles, int32_t chunk, double* work_m, double* work_c, double* m_out,
+                                 double* c_out, int32_t* cycles_out, double* dist_out, aiy_stream stream) {
+  int32_t rc = check_egm(h, dims, in);
+  if (rc) return rc;
+  if (!work_m || !work_c || !m_out || !c_out || !cycles_out || !dist_out) return fail(h, AIY_ERR_ARG, "null buffer");
+  if (max_cycles < 1) return fail(h, AIY_ERR_ARG, "max_cycles must be >= 1");
+  if (chunk <= 0) chunk = 32;
+  AIY_HIP(h, hipSetDevice(h->device));
+  rc = ensure_egm_scratch(h, dims->n_cal);
+  if (rc) return rc;
+  hipStream_t st = as_stream(stream);
+  const int n_cal = dims->n_cal;
+  const size_t per_cal = (size_t)dims->S * dims->n_M * (dims->n_a + 1);
+  const size_t buf = per_cal * n_cal;
+  EgmDev A = to_dev(dims, in);
+  AIY_HIP(h, hipMemsetAsync(h->d_dist, 0, sizeof(unsigned long long) * 3 * n_cal, st));
+  AIY_HIP(h, hipMemsetAsync(h->d_last, 0, sizeof(int) * n_cal, st));
+  const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
+  int next = 1;
+  while (true) {
+    const int end = std::min(next + chunk, last_allowed + 1);
+    for (int cyc = next; cyc < end; ++cyc) {
+      const double* mn = cyc == 1 ? nullptr : work_m + ((cyc - 1) & 1) * buf;
+      const double* cn = cyc == 1 ? nullptr : work_c + ((cyc - 1) & 1) * buf;
+      launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, cyc, h->d_dist, h->d_last, tol, st);
+    }
+    AIY_CHECK_LAUNCH(h);
+    AIY_HIP(h, hipMemcpyAsync(h->h_last, h->d_last, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipMemcpyAsync(h->h_dist, h->d_dist, sizeof(unsigned long long) * 3 * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipStreamSynchronize(st));
+    bool all = true;
+    for (int c = 0; c < n_cal; ++c) {
+      const int last = h->h_last[c];
+      double d;
+      unsigned long long bits = h->h_dist[c * 3 + last % 3];
+      memcpy(&d, &bits, sizeof(d));
+      const bool conv = (last >= 2 && !(d > tol)) || last >= last_allowed;
+      all = all && conv;
+    }
+    next = end;
+    if (all || next > last_allowed) break;
+  }
+  for (int c = 0; c < n_cal; ++c) {
+    const int last = h->h_last[c];
+    unsigned long long bits = h->h_dist[c * 3 + last % 3];
+    double d;
+    memcpy(&d, &bits, sizeof(d));
+    cycles_out[c] = last;
+    dist_out[c] = last >= 2 ? d : 100.0;
+    const size_t off = (size_t)c * per_cal;
+    AIY_HIP(h, hipMemcpyAsync(m_out + off, work_m + (last & 1) * buf + off, per_cal * sizeof(double),
+                              hipMemcpyDeviceToDevice, st));
+    AIY_HIP(h, hipMemcpyAsync(c_out + off, work_c + (last & 1) * buf + off, per_cal * sizeof(double),
+                              hipMemcpyDeviceToDevice, st));
+  }
+  AIY_HIP(h, hipStreamSynchronize(st));
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_t n_a, const double* m_tab,
+                                   const double* c_tab, const double* M_grid, const int32_t* state, const double* m,
+                                   const double* M, int64_t n, double* c_out, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (S < 1 || n_M < 1 || n_a < 2 || n < 0) return fail(h, AIY_ERR_ARG, "bad sizes");
+  if (n == 0) return AIY_OK;
+  if (!m_tab || !c_tab || !state || !m || !c_out || (n_M > 1 && (!M_grid || !M)))
+    return fail(h, AIY_ERR_ARG, "null pointer");
+  AIY_HIP(h, hipSetDevice(h->device));
+  const int tb = 256;
+  const long long nb = (n + tb - 1) / tb;
+  hipLaunchKernelGGL(policy_eval_kernel, dim3((unsigned)nb), dim3(tb), 0, as_stream(stream), S, n_M, n_a, m_tab,
+                     c_tab, M_grid, state, m, M, (long long)n, c_out);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}

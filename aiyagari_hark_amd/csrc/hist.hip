@@ -1,0 +1,274 @@
+// Young-lottery histogram (build-defined row E2) for gfx950.
+//
+// The reference only has the Monte Carlo panel; BASELINE's stationary Table II sweep
+// needs the distribution iteration of the stationary household:
+//   hist_lottery_kernel   (s, j) -> a' = m - c_s(m), m = R a_j + w l_s, lottery
+//                         (lo, weight on lo) onto a_grid; policy search is the
+//                         wave-cooperative monotone search of the EGM kernel.
+//   hist_push_kernel      T[s][d] += w * mass[s][j] for d in {lo, lo + 1}:
+//                         wave-aggregated fp64 atomics -- lanes are sorted by lo
+//                         (monotone savings policy), so a segmented shuffle-scan
+//                         merges equal destinations and only segment tails add.
+//   hist_mix_kernel       mass'[s'][j] = sum_s P[s,s'] T[s][j] (one lane per j,
+//                         S x S register contraction), sup-norm change, T zeroed.
+//   hist_K_kernel         K = sum mass * a (fixed order) after convergence.
+#include "common.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace aiy {
+
+__device__ __forceinline__ int upper_bound(const double* __restrict__ x, int lo, int hi, double q) {
+  while (lo < hi) {
+    int mid = lo + ((hi - lo) >> 1);
+    if (x[mid] <= q) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void hist_lottery_kernel(int S, int n_a, const double* __restrict__ m_tab,
+                                                           const double* __restrict__ c_tab,
+                                                           const double* __restrict__ a_grid,
+                                                           const double* __restrict__ R, const double* __restrict__ w,
+                                                           const double* __restrict__ lab, int* __restrict__ lo,
+                                                           double* __restrict__ wlo) {
+  const int cal = blockIdx.z, s = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = j < n_a;
+  const double* ag = a_grid + (size_t)cal * n_a;
+  const double aj = ag[active ? j : n_a - 1];
+  const double q = R[cal] * aj + w[cal] * lab[(size_t)cal * S + s];
+  const size_t row = ((size_t)cal * S + s) * (n_a + 1);
+  const double c = interp_row_wave(m_tab + row, c_tab + row, n_a, q, active);
+  const double ap = q - c;
+  int d = upper_bound(ag, 0, n_a, ap) - 1;        // searchsorted(a_grid, a', 'right') - 1
+  d = d < 0 ? 0 : (d > n_a - 2 ? n_a - 2 : d);
+  double wl = (ag[d + 1] - ap) / (ag[d + 1] - ag[d]);
+  wl = wl < 0.0 ? 0.0 : (wl > 1.0 ? 1.0 : wl);
+  if (active) {
+    const size_t o = ((size_t)cal * S + s) * n_a + j;
+    lo[o] = d;
+    wlo[o] = wl;
+  }
+}
+
+// Segmented (runs of equal key in adjacent active lanes) inclusive sum, Hillis-Steele
+// style; returns true on the lane that closes its run (its sum is the run total).
+// Every lane of the wave must call it.
+__device__ __forceinline__ bool seg_sum(int key, bool active, double& v) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int act = active ? 1 : 0;
+  const int pk = __shfl_up(key, 1, kWave);
+  const int pa = __shfl_up(act, 1, kWave);
+  const bool head = lane == 0 || !active || !pa || pk != key;
+  int start = head ? lane : 0;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int s2 = __shfl_up(start, o, kWave);
+    if (lane >= o) start = max(start, s2);
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const double v2 = __shfl_up(v, o, kWave);
+    if (lane - o >= start) v += v2;
+  }
+  const int nk = __shfl_down(key, 1, kWave);
+  const int na = __shfl_down(act, 1, kWave);
+  return active && (lane == kWave - 1 || !na || nk != key);
+}
+
+__global__ __launch_bounds__(256) void hist_push_kernel(int S, int n_a, const int* __restrict__ lo,
+                                                        const double* __restrict__ wlo,
+                                                        const double* __restrict__ mass, double* __restrict__ T,
+                                                        const unsigned long long* dslots, int iter, double tol) {
+  const int cal = blockIdx.z, s = blockIdx.y;
+  if (dslots && iter >= 2) {
+    const double dprev = __longlong_as_double((long long)dslots[cal * 3 + (iter - 1) % 3]);
+    if (!(dprev >= tol)) return;
+  }
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = j < n_a;
+  const size_t o = ((size_t)cal * S + s) * n_a + (active ? j : 0);
+  const int d = active ? lo[o] : -1;
+  const double mj = active ? mass[o] : 0.0;
+  const double wl = active ? wlo[o] : 0.0;
+  double* Trow = T + ((size_t)cal * S + s) * n_a;
+  double vlo = wl * mj;
+  double vhi = (1.0 - wl) * mj;
+  if (seg_sum(d, active, vlo)) unsafeAtomicAdd(&Trow[d], vlo);
+  if (seg_sum(d, active, vhi)) unsafeAtomicAdd(&Trow[d + 1], vhi);
+}
+
+template <int SMAX>
+__global__ __launch_bounds__(256) void hist_mix_kernel(int S, int n_a, const double* __restrict__ P,
+                                                       double* __restrict__ T, const double* __restrict__ mass,
+                                                       double* __restrict__ mass_out, unsigned long long* dslots,
+                                                       int* last_iter, int iter, double tol) {
+  const int cal = blockIdx.y;
+  if (dslots && iter >= 2) {
+    const double dprev = __longlong_as_double((long long)dslots[cal * 3 + (iter - 1) % 3]);
+    if (!(dprev >= tol)) return;
+  }
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = j < n_a;
+  const size_t base = (size_t)cal * S * n_a;
+  double t[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    t[s] = 0.0;
+    if (s < S && active) {
+      t[s] = T[base + (size_t)s * n_a + j];
+      T[base + (size_t)s * n_a + j] = 0.0;
+    }
+  }
+  const double* Pc = P + (size_t)cal * S * S;
+  double dmax = 0.0;
+  for (int sp = 0; sp < S; ++sp) {
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s)
+      if (s < S) acc += Pc[(size_t)s * S + sp] * t[s];
+    if (active) {
+      const size_t o = base + (size_t)sp * n_a + j;
+      dmax = nan_max(dmax, fabs(acc - mass[o]));
+      mass_out[o] = acc;
+    }
+  }
+  if (dslots) {
+    __shared__ double red[256 / kWave];
+    dmax = wave_nan_max(dmax);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = dmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double d = red[0];
+      for (int w2 = 1; w2 < (int)(blockDim.x / kWave); ++w2) d = nan_max(d, red[w2]);
+      atomicMax(&dslots[cal * 3 + iter % 3], (unsigned long long)__double_as_longlong(d));
+      if (blockIdx.x == 0) {
+        dslots[cal * 3 + (iter + 1) % 3] = 0ull;
+        last_iter[cal] = iter;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void hist_K_kernel(int S, int n_a, const double* __restrict__ mass,
+                                                     const double* __restrict__ a_grid, double* __restrict__ K) {
+  const int cal = blockIdx.x;
+  double acc = 0.0;
+  const double* ag = a_grid + (size_t)cal * n_a;
+  const double* mc = mass + (size_t)cal * S * n_a;
+  for (int idx = threadIdx.x; idx < S * n_a; idx += blockDim.x) acc += mc[idx] * ag[idx % n_a];
+  __shared__ double red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) K[cal] = red[0];
+}
+
+static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
+  if ((size_t)n_cal <= h->hist_cap) return AIY_OK;
+  if (h->d_hdist) { (void)hipFree(h->d_hdist); (void)hipFree(h->d_K); (void)hipFree(h->d_hlast); }
+  if (h->h_hdist) { (void)hipHostFree(h->h_hdist); (void)hipHostFree(h->h_K); (void)hipHostFree(h->h_hlast); }
+  h->d_hdist = nullptr; h->d_K = nullptr; h->d_hlast = nullptr;
+  h->h_hdist = nullptr; h->h_K = nullptr; h->h_hlast = nullptr; h->hist_cap = 0;
+  AIY_HIP(h, hipMalloc((void**)&h->d_hdist, sizeof(unsigned long long) * 3 * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_K, sizeof(double) * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_hlast, sizeof(int) * n_cal));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_hdist, sizeof(unsigned long long) * 3 * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_K, sizeof(double) * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_hlast, sizeof(int) * n_cal, hipHostMallocDefault));
+  h->hist_cap = n_cal;
+  return AIY_OK;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" int32_t aiy_hist_lottery(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, const double* m_tab,
+                                    const double* c_tab, const double* a_grid, const double* R, const double* w,
+                                    const double* lab, int32_t* lo, double* wlo, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (n_cal < 1 || S < 1 || n_a < 2 || n_cal > 65535 || S > 65535) return fail(h, AIY_ERR_ARG, "bad sizes");
+  if (!m_tab || !c_tab || !a_grid || !R || !w || !lab || !lo || !wlo) return fail(h, AIY_ERR_ARG, "null pointer");
+  AIY_HIP(h, hipSetDevice(h->device));
+  dim3 grid((n_a + 255) / 256, S, n_cal);
+  hipLaunchKernelGGL(hist_lottery_kernel, grid, dim3(256), 0, as_stream(stream), S, n_a, m_tab, c_tab, a_grid, R, w,
+                     lab, lo, wlo);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, const int32_t* lo,
+                                  const double* wlo, const double* P, const double* a_grid, double tol,
+                                  int32_t max_iter, int32_t chunk, double* mass, double* work, double* K_out,
+                                  int32_t* iters_out, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (n_cal < 1 || S < 1 || n_a < 2 || n_cal > 65535 || S > AIY_MAX_STATES) return fail(h, AIY_ERR_ARG, "bad sizes");
+  if (!lo || !wlo || !P || !a_grid || !mass || !work || !K_out || !iters_out) return fail(h, AIY_ERR_ARG, "null pointer");
+  if (max_iter < 1) return fail(h, AIY_ERR_ARG, "max_iter must be >= 1");
+  if (chunk <= 0) chunk = 64;
+  AIY_HIP(h, hipSetDevice(h->device));
+  int32_t rc = ensure_hist_scratch(h, n_cal);
+  if (rc) return rc;
+  hipStream_t st = as_stream(stream);
+  const size_t per = (size_t)n_cal * S * n_a;
+  double* T = work;          // [n_cal][S][n_a] push accumulator (kept zero between iterations)
+  double* alt = work + per;  // [n_cal][S][n_a] ping-pong partner of `mass`
+  AIY_HIP(h, hipMemsetAsync(T, 0, per * sizeof(double), st));
+  AIY_HIP(h, hipMemsetAsync(h->d_hdist, 0, sizeof(unsigned long long) * 3 * n_cal, st));
+  AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * n_cal, st));
+  dim3 gpush((n_a + 255) / 256, S, n_cal);
+  dim3 gmix((n_a + 255) / 256, n_cal);
+  int it = 1;
+  while (true) {
+    const int end = std::min(it + chunk, max_iter + 1);
+    for (int k = it; k < end; ++k) {
+      const double* src = (k & 1) ? mass : alt;   // iteration k reads buffer (k-1)%2, writes k%2
+      double* dst = (k & 1) ? alt : mass;
+      hipLaunchKernelGGL(hist_push_kernel, gpush, dim3(256), 0, st, S, n_a, lo, wlo, src, T, h->d_hdist, k, tol);
+      if (S <= 8)
+        hipLaunchKernelGGL(hist_mix_kernel<8>, gmix, dim3(256), 0, st, S, n_a, P, T, src, dst, h->d_hdist, h->d_hlast, k, tol);
+      else if (S <= 16)
+        hipLaunchKernelGGL(hist_mix_kernel<16>, gmix, dim3(256), 0, st, S, n_a, P, T, src, dst, h->d_hdist, h->d_hlast, k, tol);
+      else if (S <= 32)
+        hipLaunchKernelGGL(hist_mix_kernel<32>, gmix, dim3(256), 0, st, S, n_a, P, T, src, dst, h->d_hdist, h->d_hlast, k, tol);
+      else
+        hipLaunchKernelGGL(hist_mix_kernel<64>, gmix, dim3(256), 0, st, S, n_a, P, T, src, dst, h->d_hdist, h->d_hlast, k, tol);
+    }
+    AIY_CHECK_LAUNCH(h);
+    AIY_HIP(h, hipMemcpyAsync(h->h_hlast, h->d_hlast, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipMemcpyAsync(h->h_hdist, h->d_hdist, sizeof(unsigned long long) * 3 * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipStreamSynchronize(st));
+    bool all = true;
+    for (int c = 0; c < n_cal; ++c) {
+      const int last = h->h_hlast[c];
+      double d;
+      unsigned long long b = h->h_hdist[c * 3 + last % 3];
+      std::memcpy(&d, &b, sizeof(d));
+      all = all && ((last >= 1 && !(d >= tol)) || last >= max_iter);
+    }
+    it = end;
+    if (all || it > max_iter) break;
+  }
+  // bring every calibration's final distribution into `mass`
+  for (int c = 0; c < n_cal; ++c) {
+    const int last = h->h_hlast[c];
+    iters_out[c] = last;
+    if (last & 1) {
+      const size_t off = (size_t)c * S * n_a;
+      AIY_HIP(h, hipMemcpyAsync(mass + off, alt + off, (size_t)S * n_a * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+  }
+  hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(256), 0, st, S, n_a, mass, a_grid, h->d_K);
+  AIY_CHECK_LAUNCH(h);
+  AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
+  AIY_HIP(h, hipStreamSynchronize(st));
+  for (int c = 0; c < n_cal; ++c) K_out[c] = h->h_K[c];
+  return AIY_OK;
+}

@@ -1,0 +1,64 @@
+// Host-side internals shared by the libaiyagari translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/aiyagari.h"
+
+struct aiy_handle {
+  int device = 0;
+  std::string err;
+  // EGM convergence bookkeeping: [n_cal][3] distance slots (bit patterns of
+  // non-negative doubles, atomicMax) and [n_cal] last completed cycle.
+  unsigned long long* d_dist = nullptr;
+  int* d_last = nullptr;
+  size_t egm_cap = 0;
+  // host pinned mirrors
+  unsigned long long* h_dist = nullptr;
+  int* h_last = nullptr;
+  // panel: per-block partial sums
+  double* d_partials = nullptr;
+  size_t partials_cap = 0;
+  // histogram: per-calibration sup-norm slots [n_cal][3] + sums of K
+  unsigned long long* d_hdist = nullptr;
+  double* d_K = nullptr;
+  int* d_hlast = nullptr;
+  size_t hist_cap = 0;
+  unsigned long long* h_hdist = nullptr;
+  double* h_K = nullptr;
+  int* h_hlast = nullptr;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace aiy {
+
+inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  return code;
+}
+
+#define AIY_HIP(h, expr)                                                                 \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return aiy::fail((h), AIY_ERR_HIP, "%s failed: %s (%s:%d)", #expr,                \
+                       hipGetErrorString(_e), __FILE__, __LINE__);                        \
+  } while (0)
+
+#define AIY_CHECK_LAUNCH(h) AIY_HIP(h, hipGetLastError())
+
+inline hipStream_t as_stream(aiy_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace aiy

@@ -1,0 +1,363 @@
+"""Drop-in call surface of the reference: ``AiyagariType`` and
+``AiyagariEconomy`` with the same constructor dictionaries, attributes and
+solve/simulate hooks as ``Aiyagari_Support.py`` (AS), driven the way
+``Aiyagari-HARK.py`` (AH:234-258) drives them:
+
+    econ = AiyagariEconomy(**econ_dict); econ.verbose = False
+    agent = AiyagariType(**agent_dict); agent.cycles = 0
+    agent.get_economy_data(econ); econ.agents = [agent]
+    econ.make_Mrkv_history(); econ.solve()
+    econ.sow_state['Rnow'], econ.reap_state['aNow'][0], econ.sow_state['Mnow']
+    agent.solution[0].cFunc[k].xInterpolators
+
+HARK (econ-ark 0.12) is not available, so these classes do not subclass
+``HARK.AgentType`` / ``HARK.Market``; they restate the parts of those base classes
+the reference relies on (solve_agent's infinite-horizon loop, Market.solve /
+make_history / update_dynamics) on top of libaiyagari.  Every per-grid-point and
+per-agent computation runs in the HIP library; only O(S^2)-sized setup and the
+once-per-GE-iteration regression run on the host.
+"""
+from __future__ import annotations
+
+from copy import deepcopy
+
+import numpy as np
+import torch
+from scipy import stats
+
+from . import setup_math as sm
+from .egm import EgmBatch, egm_solve, egm_step
+from .interp import DeviceSolution
+from .panel import DevicePanel
+
+init_Aiyagari_agents = dict(LaborStatesNo=7, LaborAR=0.6, LaborSD=0.2, T_cycle=1, DiscFac=0.96, CRRA=1.0,
+                            LbrInd=1.0, aMin=0.001, aMax=50.0, aCount=32, aNestFac=2,
+                            MgridBase=sm.MGRID_BASE.copy(), AgentCount=140)          # AS:752-755
+
+init_Aiyagari_economy = {                                                             # AS:1525-1551
+    "verbose": True, "LaborStatesNo": 7, "LaborAR": 0.6, "LaborSD": 0.2, "act_T": 11000,
+    "T_discard": 1000, "DampingFac": 0.5, "intercept_prev": [0.0, 0.0], "slope_prev": [1.0, 1.0],
+    "DiscFac": 0.96, "CRRA": 1.0, "LbrInd": 1.0, "ProdB": 1.0, "ProdG": 1.0, "CapShare": 0.36,
+    "DeprFac": 0.08, "DurMeanB": 8.0, "DurMeanG": 8.0, "SpellMeanB": 2.5, "SpellMeanG": 1.5,
+    "UrateB": 0.0, "UrateG": 0.0, "RelProbBG": 0.75, "RelProbGB": 1.25, "MrkvNow_init": 0,
+}
+
+
+class AggregateSavingRule:
+    """AS:1973-2005: A = exp(intercept + slope * log M)."""
+
+    distance_criteria = ["slope", "intercept"]
+
+    def __init__(self, intercept, slope):
+        self.intercept = intercept
+        self.slope = slope
+
+    def __call__(self, Mnow):
+        return np.exp(self.intercept + self.slope * np.log(Mnow))
+
+    def distance(self, other):
+        return max(float(abs(self.slope - other.slope)), float(abs(self.intercept - other.intercept)))
+
+
+class AggShocksDynamicRule:
+    """AS:2008-2020; distance = max over states of the rules' distances ([HARK] MetricObject)."""
+
+    distance_criteria = ["AFunc"]
+
+    def __init__(self, AFunc):
+        self.AFunc = AFunc
+
+    def distance(self, other):
+        if len(self.AFunc) != len(other.AFunc):
+            return float(abs(len(self.AFunc) - len(other.AFunc)))
+        return max(a.distance(b) for a, b in zip(self.AFunc, other.AFunc))
+
+
+class _Terminal:
+    """update_solution_terminal (AS:892-904): cFunc = IdentityFunction(n_dims=2) for
+    every discrete state.  Represented symbolically: the device EGM treats it as the
+    cold-start guess c(m, M) = m."""
+
+    def __init__(self, S, CRRA):
+        self.S = S
+        self.CRRA = CRRA
+
+
+class AiyagariType:
+    """AS:759-1415 on libaiyagari."""
+
+    def __init__(self, device=None, shock_mode="numpy", shock_seed=0, **kwds):
+        params = init_Aiyagari_agents.copy()
+        params.update(kwds)
+        for k, v in params.items():
+            setattr(self, k, v)
+        self.params = params
+        # [HARK] AgentType defaults used by the reference
+        self.cycles = 1
+        self.tolerance = 1e-6
+        self.seed = 0
+        self.verbose = getattr(self, "verbose", False)
+        self.pseudo_terminal = False
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.shock_mode = shock_mode
+        self.shock_seed = shock_seed
+        self.time_vary = []
+        self.time_inv = ["DiscFac", "CRRA"]
+        self.state_now = {"aNow": None, "mNow": None, "EmpNow": None, "LaborSupplyState": None}
+        self.state_prev = dict(self.state_now)
+        self.shock_vars = {"Mrkv": None}
+        self.shocks = {}
+        self.controls = {}
+        self.solve_one_period = egm_step
+        self.panel = None
+        self.update()
+
+    # ---- solve side -------------------------------------------------------------------
+    def add_to_time_inv(self, *names):
+        for n in names:
+            if n not in self.time_inv:
+                self.time_inv.append(n)
+
+    def pre_solve(self):                      # AS:806-808
+        self.update()
+        self.precompute_arrays()
+
+    def update(self):                         # AS:810-815
+        self.make_grid()
+        self.update_solution_terminal()
+
+    def get_economy_data(self, Economy):      # AS:817-873
+        self.T_sim = Economy.act_T
+        self.kInit = Economy.KSS
+        self.MrkvInit = Economy.sow_init["Mrkv"]
+        self.Mgrid = Economy.MSS * np.asarray(self.MgridBase)
+        self.AFunc = Economy.AFunc
+        for name in ("DeprFac", "CapShare", "LbrInd", "UrateB", "UrateG", "ProdB", "ProdG", "MrkvIndArray",
+                     "MrkvEmplArray", "TauchenAux"):
+            setattr(self, name, getattr(Economy, name))
+        self.MrkvAggArray = Economy.MrkvArray
+        self.add_to_time_inv("Mgrid", "AFunc", "DeprFac", "CapShare", "LaborStatesNo", "LaborAR", "LaborSD",
+                             "UrateB", "LbrInd", "UrateG", "ProdB", "ProdG", "MrkvIndArray", "MrkvAggArray",
+                             "MrkvEmplArray", "TauchenAux")
+
+    def make_grid(self):                      # AS:875-890
+        self.aGrid = sm.make_grid_exp_mult(self.aMin, self.aMax, self.aCount, self.aNestFac)
+        self.add_to_time_inv("aGrid")
+        self.TauchenAux = sm.labor_tauchen(self.LaborStatesNo, self.LaborAR, self.LaborSD)
+        self.add_to_time_inv("TauchenAux")
+
+    def update_solution_terminal(self):       # AS:892-904
+        self.solution_terminal = _Terminal(4 * self.LaborStatesNo, self.CRRA)
+
+    def precompute_arrays(self):              # AS:906-1037
+        if self.UrateB != 0.0 or self.UrateG != 0.0:
+            raise NotImplementedError("UrateB/UrateG > 0 (full Krusell-Smith employment) is SURVEY §8f rank 2")
+        S = 4 * self.LaborStatesNo
+        R, W, M = sm.next_prices([f.intercept for f in self.AFunc], [f.slope for f in self.AFunc], self.Mgrid, S,
+                                 self.UrateB, self.UrateG, self.LbrInd, self.ProdB, self.ProdG, self.CapShare,
+                                 self.DeprFac)
+        self.LSStates = sm.labor_levels(self.TauchenAux[0])
+        lab = np.array([self.LSStates[sp // 4] for sp in range(S)])
+        self.egm_batch = EgmBatch.from_numpy(self.aGrid, self.Mgrid, self.MrkvIndArray, R, W, M, lab, self.DiscFac,
+                                             self.CRRA, device=self.device)
+        self.add_to_time_inv("egm_batch")
+
+    def solve(self, verbose=False):
+        """[HARK] AgentType.solve -> solve_agent (cycles = 0: infinite horizon)."""
+        if self.cycles != 0:
+            raise NotImplementedError("only the infinite-horizon solve (cycles = 0, AH:237) is on the hot path")
+        self.pre_solve()
+        m, c, cycles, dist = egm_solve(self.egm_batch, tol=self.tolerance, max_cycles=5000)
+        self.completed_cycles = int(cycles[0]) - 1
+        self.solution_distance = float(dist[0])
+        self.solution = [DeviceSolution(m[0], c[0], self.egm_batch.M_grid[0], self.CRRA)]
+        self.post_solve()
+        return self.solution
+
+    def post_solve(self):
+        pass
+
+    # ---- simulation side ---------------------------------------------------------------
+    def reset(self):                          # AS:1158
+        self.initialize_sim()
+
+    def initialize_sim(self):                 # AS:1164-1171 + [HARK] AgentType.initialize_sim
+        self.shocks["Mrkv"] = self.MrkvInit
+        emp, lab = sm.birth_states(self.AgentCount, self.LaborStatesNo, self.UrateB, seed=self.seed)
+        self.state_now["EmpNow"] = emp
+        self.state_now["LaborSupplyState"] = lab
+        self.t_sim = 0
+        if self.panel is None or self.panel.n_local != self.AgentCount or self.panel.act_T != self.T_sim:
+            self.panel = DevicePanel(self.AgentCount, device=self.device, act_T=self.T_sim)
+        self.lab_cdf = sm.choice_cdf_table(self.TauchenAux[1])          # agent's own chain (AS:1245, Q5)
+
+    def market_action(self):                  # AS:1161
+        raise NotImplementedError("per-period hooks are fused into AiyagariEconomy.make_history on device")
+
+
+class AiyagariEconomy:
+    """AS:1555-1964 on libaiyagari (Market restated)."""
+
+    def __init__(self, agents=None, tolerance=0.01, **kwds):
+        agents = agents if agents is not None else list()
+        params = deepcopy(init_Aiyagari_economy)
+        params.update(kwds)          # keeps the caller's intercept_prev/slope_prev lists (quirk Q9)
+        self.agents = agents
+        self.tolerance = tolerance
+        self.max_loops = 1000
+        self.sow_vars = ["Mnow", "Aprev", "Mrkv", "Rnow", "Wnow"]
+        self.reap_vars = ["aNow", "EmpNow"]
+        self.track_vars = ["Mrkv", "Aprev", "Mnow", "Urate"]
+        self.dyn_vars = ["AFunc"]
+        for k, v in params.items():
+            setattr(self, k, v)
+        self.sow_init = {v: None for v in self.sow_vars}
+        self.sow_state = {v: None for v in self.sow_vars}
+        self.reap_state = {v: [] for v in self.reap_vars}
+        self.history = {v: [] for v in self.track_vars}
+        self.update()
+
+    def update(self):                         # AS:1593-1629
+        self.AFunc = [AggregateSavingRule(self.intercept_prev[j], self.slope_prev[j]) for j in range(2)]
+        ss = sm.steady_state(self.CRRA, self.DiscFac, self.DeprFac, self.CapShare, self.LbrInd)
+        for k, v in ss.items():
+            setattr(self, k, v)
+        self.convertKtoY = lambda KtoY: KtoY ** (1.0 / (1.0 - self.CapShare))
+        self.rFunc = lambda k: self.CapShare * k ** (self.CapShare - 1.0)
+        self.Wfunc = lambda k: ((1.0 - self.CapShare) * k ** (self.CapShare))
+        self.sow_init.update(KtoLnow=self.KtoLSS, Mnow=self.MSS, Aprev=self.KSS, Rnow=self.RSS, Wnow=self.WSS, Mrkv=0)
+        self.make_MrkvArray()
+
+    def make_MrkvArray(self):                 # AS:1639-1791
+        agg, E = sm.employment_chain(self.DurMeanB, self.DurMeanG, self.SpellMeanB, self.SpellMeanG, self.UrateB,
+                                     self.UrateG, self.RelProbBG, self.RelProbGB)
+        T = sm.labor_tauchen(self.LaborStatesNo, self.LaborAR, self.LaborSD)
+        self.MrkvArray = agg
+        self.MrkvEmplArray = E
+        self.MrkvIndArray = sm.kron_states(T[1], E)
+        self.TauchenAux = T
+
+    def make_Mrkv_history(self):              # AS:1793-1805
+        self.MrkvNow_hist = sm.markov_history(self.MrkvArray, self.act_T, self.MrkvNow_init, seed=0)
+
+    def reset(self):                          # AS:1631-1637 + [HARK] Market.reset
+        self.Shk_idx = 0
+        self.history = {v: [] for v in self.track_vars}
+        for v in self.sow_state:
+            self.sow_state[v] = self.sow_init[v]
+        for a in self.agents:
+            a.reset()
+
+    # ---- GE fixed point ----------------------------------------------------------------
+    def solve_agents(self):
+        for a in self.agents:
+            a.solve()
+
+    def make_history(self):
+        """[HARK] Market.make_history: act_T periods of sow -> cultivate -> reap -> mill ->
+        store, fused on device (libaiyagari aiy_sim_periods)."""
+        if len(self.agents) != 1:
+            raise NotImplementedError("the reference economy has exactly one AgentType")
+        agent = self.agents[0]
+        self.reset()
+        p = agent.panel
+        sol = agent.solution[0]
+        lab_level = torch.as_tensor(agent.LSStates if hasattr(agent, "LSStates") else
+                                    sm.labor_levels(agent.TauchenAux[0]), dtype=torch.float64).to(agent.device)
+        lab_cdf = torch.as_tensor(agent.lab_cdf, dtype=torch.float64).to(agent.device)
+        hist = torch.as_tensor(np.asarray(self.MrkvNow_hist, dtype=np.int32)).to(agent.device)
+        market = dict(CapShare=self.CapShare, DeprFac=self.DeprFac, prod=(self.ProdB, self.ProdG),
+                      agg_L=((1.0 - self.UrateB) * self.LbrInd, (1.0 - self.UrateG) * self.LbrInd))
+        p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, hist, market)
+        p.reset(agent.kInit, agent.state_now["LaborSupplyState"], self.sow_init["Mnow"], self.sow_init["Aprev"],
+                self.sow_init["Mrkv"], self.sow_init["Rnow"], self.sow_init["Wnow"])
+        ge_iter = getattr(self, "_ge_iter", 0)
+        if agent.shock_mode == "numpy":
+            N = agent.AgentCount
+            src = lambda n: np.random.random_sample((n, N))  # noqa: E731 -- the reference's global RNG
+            p.run(0, self.act_T, shock_mode="numpy", u_host_source=src, ge_iter=ge_iter)
+        else:
+            p.run(0, self.act_T, shock_mode="philox", seed=agent.shock_seed, ge_iter=ge_iter)
+        torch.cuda.synchronize(agent.device)
+        self.Shk_idx = self.act_T
+        s = p.sow_host()
+        for v in self.sow_vars:
+            self.sow_state[v] = s[v]
+        aNow = p.a.cpu().numpy()
+        self.reap_state = {"aNow": [aNow], "EmpNow": [np.ones(agent.AgentCount)]}
+        agent.state_now["aNow"] = aNow
+        agent.state_now["LaborSupplyState"] = p.lab.cpu().numpy().astype(np.int64)
+        self.history = {"Mrkv": list(np.asarray(self.MrkvNow_hist[:self.act_T])),
+                        "Aprev": p.hist_A.cpu().numpy(), "Mnow": p.hist_M.cpu().numpy(),
+                        "Urate": np.zeros(self.act_T)}
+
+    def update_dynamics(self):                # [HARK] Market.update_dynamics
+        dyn = self.calc_dynamics(Mnow=self.history["Mnow"], Aprev=self.history["Aprev"])
+        for v in self.dyn_vars:
+            for a in self.agents:
+                setattr(a, v, getattr(dyn, v))
+        return dyn
+
+    def solve(self):                          # [HARK] Market.solve
+        go = True
+        loops = 0
+        old = None
+        self.ge_log = []
+        while go:
+            self._ge_iter = loops
+            self.solve_agents()
+            self.make_history()
+            new = self.update_dynamics()
+            distance = new.distance(old) if loops > 0 else 1000000.0
+            self.ge_log.append(dict(iter=loops, cycles=self.agents[0].completed_cycles + 1,
+                                    intercept=list(self.intercept_prev), slope=list(self.slope_prev),
+                                    distance=distance, Rnow=self.sow_state["Rnow"]))
+            old = new
+            loops += 1
+            go = distance >= self.tolerance and loops < self.max_loops
+        self.dynamics = new
+
+    # ---- market hooks (AS:1808-1964) ---------------------------------------------------
+    def mill_rule(self, aNow, EmpNow):
+        return self.calc_R_and_W(aNow, EmpNow)
+
+    def calc_dynamics(self, Mnow, Aprev):
+        return self.calc_AFunc(Mnow, Aprev)
+
+    def calc_R_and_W(self, aNow, EmpNow):
+        """AS:1839-1894 for one period given the agents' assets (scalar formulas; the
+        device path fuses this into aiy_sim_periods)."""
+        Aprev = float(np.mean(np.array(aNow)))
+        Urate = 1.0 - float(np.mean(np.array(EmpNow)))
+        self.Urate = Urate
+        Mrkv = self.MrkvNow_hist[self.Shk_idx]
+        Prod, L = (self.ProdB, (1.0 - self.UrateB) * self.LbrInd) if Mrkv == 0 else \
+            (self.ProdG, (1.0 - self.UrateG) * self.LbrInd)
+        self.Shk_idx += 1
+        k = Aprev / L
+        R = 1.0 + Prod * self.rFunc(k) - self.DeprFac
+        W = Prod * self.Wfunc(k)
+        self.KtoLnow = k
+        return R * Aprev + W * L, Aprev, Mrkv, R, W
+
+    def calc_AFunc(self, Mnow, Aprev):
+        """AS:1896-1964: per-state OLS of log A_t on log M_{t-1} after T_discard, damped."""
+        T = len(Mnow)
+        d = self.T_discard
+        w = 1.0 - self.DampingFac
+        logA = np.log(np.asarray(Aprev)[d:T])
+        logM = np.log(np.asarray(Mnow)[d - 1:T - 1])
+        hist = np.asarray(self.MrkvNow_hist)[d - 1:T - 1]
+        rules, rsq = [], []
+        for i in range(self.MrkvArray.shape[0]):
+            these = i == hist
+            res = stats.linregress(logM[these], logA[these])
+            intercept = w * res.intercept + (1.0 - w) * self.intercept_prev[i]
+            slope = w * res.slope + (1.0 - w) * self.slope_prev[i]
+            rules.append(AggregateSavingRule(intercept, slope))
+            rsq.append(res.rvalue ** 2)
+            self.intercept_prev[i] = intercept
+            self.slope_prev[i] = slope
+        if self.verbose:
+            print("intercept=" + str(self.intercept_prev) + ", slope=" + str(self.slope_prev) + ", r-sq=" + str(rsq))
+        return AggShocksDynamicRule(rules)

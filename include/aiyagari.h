@@ -1,0 +1,181 @@
+/*
+ * libaiyagari -- C ABI of the MI355X (gfx950) Aiyagari household block.
+ *
+ * Drop-in boundary for the hot path of Dostenlinus/Aiyagari-HARK:
+ *   EGM backward step -> cross-sectional step (panel / histogram) -> GE loop.
+ * Every entry point cites the reference interface it replaces
+ * (AS = /root/reference/Aiyagari_Support.py, AH = /root/reference/Aiyagari-HARK.py,
+ * [HARK] = econ-ark 0.12 library routine called from there).
+ *
+ * Conventions
+ *  - All array arguments are DEVICE pointers owned by the caller (the Python host
+ *    allocates them as PyTorch-ROCm tensors); the library allocates only inside a
+ *    handle (small scratch).  Layouts are C-contiguous, float64 unless stated.
+ *  - Every call returns 0 (AIY_OK) or a negative error code; aiy_last_error() gives
+ *    the message.  Argument errors are detected on the host before any launch.
+ *  - `stream` is a hipStream_t (NULL = the default stream).  Calls that only enqueue
+ *    work are asynchronous; calls documented as BLOCKING synchronise `stream`.
+ *  - One handle per (process, device); a handle is not re-entrant across threads.
+ *
+ * Table layout for consumption policies (the (x_list, y_list) of the reference's
+ * 28 x 15 LinearInterp objects, AS:1509-1516):
+ *    m[c][s][k][j], c[c][s][k][j]   c < n_cal, s < S, k < n_M, j <= n_a
+ * where node j = 0 is the prepended (1e-7, 1e-7) point (AS:1503-1504).
+ */
+#ifndef AIYAGARI_H
+#define AIYAGARI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIY_OK 0
+#define AIY_ERR_ARG (-1)
+#define AIY_ERR_HIP (-2)
+#define AIY_ERR_STATE (-3)
+#define AIY_ERR_UNSUPPORTED (-4)
+#define AIY_ERR_COMM (-5)
+
+#define AIY_MAX_STATES 64   /* S (discrete states) supported by the EGM kernel */
+
+typedef struct aiy_handle aiy_handle;
+typedef void* aiy_stream; /* hipStream_t */
+
+/* Shapes of one batched EGM problem. */
+typedef struct {
+  int32_t n_cal; /* calibrations solved together (Table II batching)                 */
+  int32_t S;     /* discrete states: 4 * LaborStatesNo (KS form) or N_l (stationary)  */
+  int32_t n_M;   /* aggregate-M nodes (15 in the reference, AS:753-754); 1 = stationary */
+  int32_t n_a;   /* exogenous end-of-period asset nodes (aGrid, AS:880)               */
+} aiy_egm_dims;
+
+/* Per-calibration inputs of solve_Aiyagari (AS:1423-1434) after precompute_arrays
+ * (AS:906-1037) with the 28x-redundant current-state axis removed:
+ *   mNextArray[a,k,s,s'] = R_next[k,s'] * a_grid[a] + W_next[k,s'] * lab[s']
+ *   MnextArray[a,k,s,s'] = M_next[k,s'],  RnextArray[a,k,s,s'] = R_next[k,s'],
+ *   ProbArray[a,k,s,s']  = P[s,s'].                                                  */
+typedef struct {
+  const double* a_grid; /* [n_cal][n_a]                                           */
+  const double* M_grid; /* [n_cal][n_M]   Mgrid = MSS * MgridBase (AS:837-839)     */
+  const double* P;      /* [n_cal][S][S]  MrkvIndArray (AS:1780)                    */
+  const double* R_next; /* [n_cal][n_M][S]                                          */
+  const double* W_next; /* [n_cal][n_M][S]                                          */
+  const double* M_next; /* [n_cal][n_M][S] (ignored when n_M == 1)                  */
+  const double* lab;    /* [n_cal][S]     LSStates[s' / 4] (AS:985, 990-1018)       */
+  const double* beta;   /* [n_cal]        DiscFac                                  */
+  const double* crra;   /* [n_cal]        CRRA                                     */
+} aiy_egm_inputs;
+
+/* Library version (major * 10000 + minor * 100 + patch). */
+int32_t aiy_version(void);
+
+/* Create / destroy a handle bound to HIP device `device`. */
+int32_t aiy_create(int32_t device, aiy_handle** out);
+int32_t aiy_destroy(aiy_handle* h);
+const char* aiy_last_error(const aiy_handle* h);
+
+/* One backward EGM step == one call of solve_Aiyagari (AS:1423-1520) for every
+ * calibration of the batch.  m_next/c_next == NULL means the terminal guess
+ * IdentityFunction (AS:892-904).  Asynchronous. */
+int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
+                     const double* m_next, const double* c_next, double* m_out, double* c_out,
+                     aiy_stream stream);
+
+/* Infinite-horizon solve == [HARK] solve_agent with cycles = 0 (AH:237): cold start
+ * from the terminal guess (pre_solve, AS:806-808), iterate solve_Aiyagari until the
+ * [HARK] MetricObject distance (max |dm|, |dc| over all tables) is <= tol, or
+ * max_cycles + 1 cycles ran (HARK's 5000-cycle escape clause).  Each calibration
+ * stops on its own cycle; converged calibrations are skipped on device.
+ *   work_m/work_c: [2][n_cal][S][n_M][n_a+1] ping-pong scratch (caller-owned)
+ *   m_out/c_out:   [n_cal][S][n_M][n_a+1] converged tables
+ *   cycles_out/dist_out: HOST arrays [n_cal] (completed cycles, final distance)
+ * BLOCKING (polls convergence every `chunk` cycles; chunk <= 0 selects 32). */
+int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                      int32_t max_cycles, int32_t chunk, double* work_m, double* work_c,
+                      double* m_out, double* c_out, int32_t* cycles_out, double* dist_out,
+                      aiy_stream stream);
+
+/* cFunc[state](m, M) for a batch of queries (interop for .solution[0].cFunc and the
+ * notebook's plots, AH:271-275): HARK LinearInterpOnInterp1D semantics.
+ *   tables [S][n_M][n_a+1]; state/m/M [n]; c_out [n].  Asynchronous. */
+int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_t n_a, const double* m_tab,
+                        const double* c_tab, const double* M_grid, const int32_t* state,
+                        const double* m, const double* M, int64_t n, double* c_out, aiy_stream stream);
+
+/* ----------------------------- panel (rows B1-B6, C2) ----------------------------- */
+
+/* Market constants used by calc_R_and_W (AS:1839-1894). */
+typedef struct {
+  double cap_share;  /* CapShare */
+  double depr_fac;   /* DeprFac */
+  double prod[2];    /* ProdB, ProdG */
+  double agg_L[2];   /* (1 - UrateB) LbrInd, (1 - UrateG) LbrInd */
+} aiy_market;
+
+/* Household panel model for one calibration (policy fixed during a history). */
+typedef struct {
+  int32_t S, n_M, n_a, n_lab;
+  const double* m_pol;     /* [S][n_M][n_a+1] converged policy (AiyagariType.solution[0]) */
+  const double* c_pol;     /* [S][n_M][n_a+1]                                             */
+  const double* M_grid;    /* [n_M]                                                       */
+  const double* lab_level; /* [n_lab] LSStates (AS:1265)                                  */
+  const double* lab_cdf;   /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
+  const int32_t* mrkv_hist;/* [act_T] MrkvNow_hist (AS:1793-1805)                          */
+} aiy_panel_model;
+
+/* Device-resident market state ("sow_state", AS:1585), 8 doubles:
+ *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] local sum(a) [7] reserved */
+#define AIY_SOW_DOUBLES 8
+
+/* Simulate periods t0 .. t0 + n_periods - 1 of Market.make_history (AH:249 ->
+ * [HARK] Market.make_history): for each period one [HARK] sim_one_period of every
+ * local agent (get_shocks AS:1217-1256, get_states AS:1259-1283, get_controls
+ * AS:1286-1409, get_poststates AS:1411-1415), then mill/calc_R_and_W (AS:1839-1894)
+ * on the mean of `a` over all n_total agents of all ranks, writing sow and
+ * hist_A[t] = Aprev, hist_M[t] = Mnow (the track_vars of AS:1587).
+ *   a [n_local] (in: a_prev, out: a_now), lab [n_local] uint8 labour state
+ *   u: NULL -> on-device Philox4x32-10 (counter (ge_iter<<20 | t, idx, 0), key seed),
+ *      else host-supplied uniforms [n_periods][u_ld] (parity with np.random.choice)
+ *   agent_offset: global index of local agent 0 (Philox counter, sharding)
+ * With a communicator bound (aiy_comm_init) the per-period sum of a is all-reduced
+ * over RCCL before the prices are formed.  Asynchronous. */
+int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
+                        int64_t n_local, int64_t agent_offset, int64_t n_total, double* a,
+                        uint8_t* lab, const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter,
+                        int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
+                        aiy_stream stream);
+
+/* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
+/* 128-byte ncclUniqueId created by rank 0 and broadcast by the host. */
+int32_t aiy_comm_unique_id(void* out128);
+int32_t aiy_comm_init(aiy_handle* h, const void* unique_id128, int32_t nranks, int32_t rank);
+int32_t aiy_comm_destroy(aiy_handle* h);
+/* Sum-all-reduce of n doubles in place over the bound communicator (asynchronous). */
+int32_t aiy_allreduce_sum(aiy_handle* h, double* buf, int64_t n, aiy_stream stream);
+
+/* --------------------- stationary extensions (E1 / E2, no reference) --------------------- */
+
+/* Young-lottery transition of each calibration's stationary household (build-defined
+ * row E2): for state s and grid node j, m = R a_j + w lab[s], a' = m - c_s(m) (HARK
+ * LinearInterp on the [S][n_a+1] tables), lottery onto a_grid:
+ * lo[c][s][j] (int32) and wlo (weight on lo).  Asynchronous. */
+int32_t aiy_hist_lottery(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, const double* m_tab,
+                         const double* c_tab, const double* a_grid, const double* R, const double* w,
+                         const double* lab, int32_t* lo, double* wlo, aiy_stream stream);
+
+/* Iterate mass'[s', .] = sum_s P[s, s'] * lottery_push(mass[s, .]) until the sup-norm
+ * change is < tol (per calibration) or max_iter.  mass [n_cal][S][n_a] in/out,
+ * work [2][n_cal][S][n_a] scratch.  K_out (HOST [n_cal]) = sum mass * a_grid;
+ * iters_out (HOST [n_cal]).  BLOCKING. */
+int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, const int32_t* lo,
+                       const double* wlo, const double* P, const double* a_grid, double tol,
+                       int32_t max_iter, int32_t chunk, double* mass, double* work, double* K_out,
+                       int32_t* iters_out, aiy_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIYAGARI_H */

@@ -1,0 +1,86 @@
+"""CPU tests of the C-ABI boundary: the library builds/loads, exports every entry point
+include/aiyagari.h declares, the ctypes layer binds all of them, and host-side argument
+validation rejects bad calls before any device work (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "aiyagari.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(aiy_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from aiyagari_hark_amd import build, _lib
+    build.build(verbose=False)
+    return _lib.load()
+
+
+def test_header_lists_expected_entry_points():
+    fns = header_functions()
+    for must in ("aiy_create", "aiy_destroy", "aiy_egm_step", "aiy_egm_solve", "aiy_sim_periods",
+                 "aiy_hist_lottery", "aiy_hist_solve", "aiy_comm_init", "aiy_allreduce_sum", "aiy_policy_eval"):
+        assert must in fns
+
+
+def test_library_exports_every_header_symbol(lib):
+    import subprocess
+    from aiyagari_hark_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (aiy_\w+)", out))
+    assert set(header_functions()) <= exported
+    assert set(_lib.exported_symbols()) == set(header_functions())
+    for name in header_functions():
+        assert getattr(lib, name) is not None
+
+
+def test_library_targets_gfx950():
+    from aiyagari_hark_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_struct_layouts(lib):
+    from aiyagari_hark_amd import _lib
+    assert ctypes.sizeof(_lib.EgmDims) == 16
+    assert ctypes.sizeof(_lib.EgmInputs) == 9 * 8
+    assert ctypes.sizeof(_lib.Market) == 6 * 8
+    assert ctypes.sizeof(_lib.PanelModel) == 16 + 6 * 8
+
+
+def test_argument_validation_without_gpu(lib):
+    from aiyagari_hark_amd import _lib
+    assert lib.aiy_version() == 100
+    # null handle -> AIY_ERR_ARG, nothing launched
+    d = _lib.EgmDims(1, 28, 15, 32)
+    i = _lib.EgmInputs()
+    assert lib.aiy_egm_step(None, ctypes.byref(d), ctypes.byref(i), None, None, None, None, None) == -1
+    assert lib.aiy_create(0, None) == -1
+    assert lib.aiy_comm_unique_id(None) == -1
+    assert lib.aiy_destroy(None) == 0
+    assert lib.aiy_last_error(None) == b"null handle"
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+    from aiyagari_hark_amd import _lib
+    with pytest.raises(_lib.AiyagariLibError):
+        _lib.ptr(torch.zeros(3, dtype=torch.float64))
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from aiyagari_hark_amd import _lib
+    saved = _lib._lib
+    _lib._lib = None
+    try:
+        with pytest.raises(_lib.AiyagariLibError):
+            _lib.load(str(tmp_path / "nope.so"))
+    finally:
+        _lib._lib = saved

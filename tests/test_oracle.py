@@ -1,0 +1,182 @@
+"""CPU tests of the oracle (oracle/): pinned to the reference's closed forms, NumPy's own
+RNG semantics, published KAT vectors, and the committed golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+from scipy import stats
+
+from oracle import hark_ks as H
+from oracle import philox as PX
+from oracle import stationary as ST
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_steady_state_closed_forms():
+    # KSS, MSS for config 1; RSS = 1 / beta
+    ss = H.steady_state(H.INIT_ECONOMY)
+    assert ss["KSS"] == pytest.approx(5.446807380113233, rel=1e-15)
+    assert ss["MSS"] == pytest.approx(6.851881950575776, rel=1e-15)
+    assert ss["RSS"] == pytest.approx(1 / 0.96, rel=1e-14)
+
+
+def test_table2_identity():
+    # s = delta K/Y = delta alpha / (r + delta); r = 4.1666 % -> 23.67 %
+    r, a, d = 0.041666, 0.36, 0.08
+    assert d * a / (r + d) == pytest.approx(0.2367, abs=5e-5)
+
+
+def test_grid_and_tauchen():
+    g = H.make_grid_exp_mult(0.001, 50.0, 32, 2)
+    assert g[0] == pytest.approx(0.001, rel=1e-12) and g[-1] == pytest.approx(50.0, rel=1e-12)
+    assert np.all(np.diff(g) > 0)
+    y, P = H.tauchen_for(7, 0.6, 0.2)
+    assert np.allclose(P.sum(1), 1.0, atol=1e-15)
+    assert y[-1] == pytest.approx(3 * 0.2, rel=1e-12)     # yN = 3 sigma_y
+    assert np.allclose(y, -y[::-1])
+
+
+def test_markov_kron():
+    mk = H.make_MrkvArray(H.INIT_ECONOMY)
+    P7 = mk["TauchenAux"][1]
+    E4 = mk["MrkvEmplArray"]
+    assert np.array_equal(mk["MrkvIndArray"], np.kron(P7, E4))
+    assert np.allclose(mk["MrkvIndArray"].sum(1), 1.0, atol=1e-14)
+    assert np.allclose(mk["MrkvArray"], [[7 / 8, 1 / 8], [1 / 8, 7 / 8]])
+    # Urate = 0: employed rows of each aggregate block carry the whole block probability
+    assert E4[1, 0] == 0.0 and E4[3, 2] == 0.0
+
+
+def test_linear_interp_semantics():
+    f = H.LinearInterp([1.0, 2.0, 4.0], [10.0, 20.0, 30.0])
+    out = f(np.array([0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0]))
+    assert np.isnan(out[0])                          # below the grid: NaN (lower_extrap=False)
+    assert np.allclose(out[1:], [10, 15, 20, 25, 30, 40])   # linear extrapolation above
+    g = H.LinearInterpOnInterp1D([H.LinearInterp([0, 1], [0, 1]), H.LinearInterp([0, 1], [0, 2])], [1.0, 2.0])
+    assert g(np.array([0.5, 0.5, 0.5]), np.array([1.0, 1.5, 3.0])).tolist() == [0.5, 0.75, 1.5]
+
+
+def test_egm_literal_vs_vectorised_bit_identical():
+    for crra in (1.0, 5.0):
+        m = H.KSModel(dict(CRRA=crra, LaborAR=0.9, LaborSD=0.4), dict(CRRA=crra, LaborAR=0.9, LaborSD=0.4))
+        m.AFunc = [H.AggregateSavingRule(0.3, 0.85), H.AggregateSavingRule(0.32, 0.84)]
+        arr = H.precompute_arrays_ref(m.aGrid, m.Mgrid, m.AFunc, m.LSStates, m.MrkvIndArray, m.e)
+        sol = H.terminal_solution(28, crra)
+        Rk, Wk, Mk = H.next_prices(m.AFunc, m.Mgrid, 7, m.e)
+        mt = ct = None
+        for _ in range(3):
+            sol = H.solve_Aiyagari_ref(sol, 0.96, crra, m.aGrid, m.Mgrid, arr["mNextArray"], arr["MnextArray"],
+                                       arr["ProbArray"], arr["RnextArray"], 7)
+            mt, ct = H.egm_step(mt, ct, 0.96, crra, m.aGrid, m.Mgrid, Rk, Wk, Mk, m.LSStates, m.MrkvIndArray)
+            mr, cr = H.solution_to_tables(sol)
+            assert np.array_equal(mr, mt) and np.array_equal(cr, ct)
+
+
+def test_solve_agent_literal_vs_vectorised():
+    m = H.KSModel()
+    arr = H.precompute_arrays_ref(m.aGrid, m.Mgrid, m.AFunc, m.LSStates, m.MrkvIndArray, m.e)
+    sol, cyc, d = H.solve_agent_ref(0.96, 1.0, m.aGrid, m.Mgrid, arr, 7)
+    mt, ct, cyc2, d2 = m.solve_agent()
+    mr, cr = H.solution_to_tables(sol)
+    assert cyc == cyc2 and d == d2
+    assert np.array_equal(mr, mt) and np.array_equal(cr, ct)
+
+
+def test_choice_restatement_matches_numpy_choice():
+    # get_shocks (AS:1253-1254) uses np.random.choice(7, p=P[l]); the oracle replays it from
+    # the same uniforms: compare against NumPy's own choice on identical RandomStates.
+    y, P = H.tauchen_for(7, 0.9, 0.4)
+    cdf = np.array([H.choice_cdf(r) for r in P])
+    lab = np.random.RandomState(3).randint(0, 7, size=2000)
+    r1, r2 = np.random.RandomState(99), np.random.RandomState(99)
+    ref = np.array([r1.choice(range(7), size=None, replace=True, p=P[l]) for l in lab])
+    u = r2.random_sample(lab.size)
+    assert np.array_equal(H.draw_labor(lab, u, cdf), ref)
+
+
+def test_mrkv_history_matches_markov_process_choice():
+    agg = np.array([[7 / 8, 1 / 8], [1 / 8, 7 / 8]])
+    h = H.make_Mrkv_history(agg, 3000, 0, seed=0)
+    rng = np.random.RandomState(0)
+    cdf = np.cumsum(agg, axis=1)
+    now, ref = 0, []
+    for _ in range(3000):
+        ref.append(now)
+        now = int(np.searchsorted(cdf[now] / cdf[now][-1], rng.random_sample(), side="right"))
+    assert h.tolist() == ref
+    assert 0.3 < h.mean() < 0.7
+
+
+def test_birth_permutations():
+    emp, lab = H.sim_birth_labor(700, 7, 0.0, seed=0)
+    assert emp.all() and np.bincount(lab).tolist() == [100] * 7
+    rng = np.random.RandomState(0)
+    rng.permutation(np.ones(700, dtype=bool))
+    assert np.array_equal(lab, rng.permutation(np.repeat(np.arange(7), 100)))
+
+
+def test_philox_kat():
+    # Random123 kat_vectors for philox4x32_10
+    cases = [((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+             ((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF), (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+             ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+              (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1))]
+    for c, k, want in cases:
+        got = PX.philox4x32_10(*[np.array([v], dtype=np.uint32) for v in c], *k)
+        assert [int(g[0]) for g in got] == list(want)
+    u = PX.uniform(5, np.arange(100000), 42)
+    assert 0 <= u.min() and u.max() < 1 and abs(u.mean() - 0.5) < 0.005
+
+
+def test_linregress_is_scipy():
+    x = np.log(np.linspace(5, 8, 100))
+    y = 0.1 + 0.95 * x
+    r = stats.linregress(x, y)
+    assert r.slope == pytest.approx(0.95) and r.intercept == pytest.approx(0.1)
+
+
+def test_golden_fixtures_reproduce():
+    from tests.golden import make_golden as G
+    fx = np.load(os.path.join(GOLD, "egm_cfg1.npz"))
+    now = G.egm_fixture("cfg1")
+    for k in ("m", "c", "P", "aGrid", "Mgrid", "Rk", "Wk", "Mk"):
+        assert np.array_equal(fx[k], now[k]), k
+    assert int(fx["cycles"]) == now["cycles"]
+    p = np.load(os.path.join(GOLD, "panel_cfg1.npz"))
+    pn = G.panel_fixture("cfg1")
+    assert np.array_equal(p["hist_A"], pn["hist_A"]) and np.array_equal(p["lab_final"], pn["lab_final"])
+
+
+def test_rouwenhorst_moments():
+    y, P = ST.rouwenhorst(25, 0.9, 0.4)
+    assert np.allclose(P.sum(1), 1.0, atol=1e-14)
+    w, v = np.linalg.eig(P.T)
+    pi = np.real(v[:, np.argmin(abs(w - 1))])
+    pi /= pi.sum()
+    mean = pi @ y
+    var = pi @ (y - mean) ** 2
+    assert var == pytest.approx(0.16, rel=1e-10)
+    ac = (pi * (y - mean)) @ (P @ (y - mean)) / var
+    assert ac == pytest.approx(0.9, rel=1e-10)
+
+
+def test_stationary_lottery_conserves_mass():
+    fx = np.load(os.path.join(GOLD, "stationary.npz"))
+    assert fx["mass"].sum() == pytest.approx(1.0, abs=1e-12)
+    assert fx["mass"].min() >= 0
+    r = float(fx["r"])
+    w, Kd = ST.prices(r, 0.36, 0.08)
+    assert 0 < float(fx["K"]) < 50
+
+
+def test_ge_short_run_oracle_anchor():
+    """Reduced KS fixed point (act_T = 1500) runs, converges and stays near RSS."""
+    m = H.KSModel(dict(act_T=1500, T_discard=500), dict(AgentCount=350))
+    src = H.numpy_global_u_source(7, 350)
+    log = []
+    m.solve(src, log=log)
+    res = m.results()
+    assert len(log) >= 2
+    assert 0.02 < res["r"] < 0.05
+    assert res["saving_rate"] == pytest.approx(0.08 * 0.36 / (res["r"] + 0.08), rel=0.05)
