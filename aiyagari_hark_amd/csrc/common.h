@@ -18,6 +18,26 @@ constexpr int kWave = 64;
 constexpr double kBorrowNode = 0.0000001;  // Aiyagari_Support.py:1503-1504
 
 // ---------------------------------------------------------------------------------
+// Cross-kernel control words (convergence slots, the device market state) are read
+// with agent-scope atomic loads.  A plain load of a block-uniform address compiles to
+// s_load through the scalar cache, which is not kept coherent with the vector-memory
+// atomics and stores of the previous kernels: measured on MI355X, a solve whose
+// convergence slot was read with s_load kept iterating ~20 cycles past convergence.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long load_u64_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_f64_agent(const double* p) {
+  return __longlong_as_double((long long)load_u64_agent(reinterpret_cast<const unsigned long long*>(p)));
+}
+__device__ __forceinline__ void store_u64_agent(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_f64_agent(double* p, double v) {
+  store_u64_agent(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
+}
+
+// ---------------------------------------------------------------------------------
 // Wave-level helpers
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_min(double v) {

@@ -30,6 +30,7 @@
 namespace aiy {
 
 constexpr int kEgmBlock = 128;
+constexpr int kSlots = 4;  // per-calibration convergence words
 
 struct EgmDev {
   int n_cal, S, n_M, n_a;
@@ -44,11 +45,12 @@ struct EgmDev {
   const double* crra;
 };
 
-// Convergence protocol (solve mode, dist_slots != nullptr): cycle n reads slot
-// (n-1)%3 and returns at once if cycle n-1 already met !(d > tol) (HARK:
-// go = distance > tolerance), folds its own distance into slot n%3, and zeroes
-// slot (n+1)%3 for cycle n+1.  A skipped cycle writes nothing, so every later cycle
-// also sees a zero slot and skips: convergence is sticky without host involvement.
+// Convergence protocol (solve mode, dist_slots != nullptr), per calibration 4 words:
+// three rotating distance slots and a sticky "converged" flag.  Cycle n returns at
+// once if the flag is set or if cycle n-1 met !(d > tol) (HARK: go = distance >
+// tolerance; it then sets the flag), folds its own distance into slot n%3 and zeroes
+// slot (n+1)%3 for cycle n+1.  Nothing is written after convergence, so slot
+// (last % 3) keeps the final distance for the host.
 template <int SMAX, bool TERMINAL>
 __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const double* __restrict__ m_next,
                                                               const double* __restrict__ c_next,
@@ -59,8 +61,13 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
   const int cal = blockIdx.z;
   const int k = blockIdx.y;
   if (dist_slots != nullptr && cycle >= 3) {
-    const double dprev = __longlong_as_double((long long)dist_slots[cal * 3 + (cycle - 1) % 3]);
-    if (!(dprev > tol)) return;
+    unsigned long long* slots = dist_slots + cal * kSlots;
+    if (load_u64_agent(&slots[3]) != 0ull) return;   // converged earlier (sticky flag)
+    const double dprev = __longlong_as_double((long long)load_u64_agent(&slots[(cycle - 1) % 3]));
+    if (!(dprev > tol)) {
+      if (blockIdx.x == 0 && k == 0 && threadIdx.x == 0) store_u64_agent(&slots[3], 1ull);
+      return;
+    }
   }
   const int S = A.S, n_M = A.n_M, n_a = A.n_a, n1 = n_a + 1;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -140,11 +147,11 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
       if (threadIdx.x == 0) {
         double d = red[0];
         for (int w = 1; w < (int)(blockDim.x / kWave); ++w) d = nan_max(d, red[w]);
-        atomicMax(&dist_slots[cal * 3 + cycle % 3], (unsigned long long)__double_as_longlong(d));
+        atomicMax(&dist_slots[cal * kSlots + cycle % 3], (unsigned long long)__double_as_longlong(d));
       }
     }
     if (blockIdx.x == 0 && k == 0 && threadIdx.x == 0) {
-      dist_slots[cal * 3 + (cycle + 1) % 3] = 0ull;
+      store_u64_agent(&dist_slots[cal * kSlots + (cycle + 1) % 3], 0ull);
       last_cycle[cal] = cycle;
     }
   }
@@ -221,9 +228,9 @@ static int32_t ensure_egm_scratch(aiy_handle* h, int n_cal) {
   if (h->d_dist) { (void)hipFree(h->d_dist); (void)hipFree(h->d_last); }
   if (h->h_dist) { (void)hipHostFree(h->h_dist); (void)hipHostFree(h->h_last); }
   h->d_dist = nullptr; h->d_last = nullptr; h->h_dist = nullptr; h->h_last = nullptr; h->egm_cap = 0;
-  AIY_HIP(h, hipMalloc((void**)&h->d_dist, sizeof(unsigned long long) * 3 * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_dist, sizeof(unsigned long long) * kSlots * n_cal));
   AIY_HIP(h, hipMalloc((void**)&h->d_last, sizeof(int) * n_cal));
-  AIY_HIP(h, hipHostMalloc((void**)&h->h_dist, sizeof(unsigned long long) * 3 * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_dist, sizeof(unsigned long long) * kSlots * n_cal, hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_last, sizeof(int) * n_cal, hipHostMallocDefault));
   h->egm_cap = n_cal;
   return AIY_OK;
@@ -263,7 +270,7 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   const size_t per_cal = (size_t)dims->S * dims->n_M * (dims->n_a + 1);
   const size_t buf = per_cal * n_cal;
   EgmDev A = to_dev(dims, in);
-  AIY_HIP(h, hipMemsetAsync(h->d_dist, 0, sizeof(unsigned long long) * 3 * n_cal, st));
+  AIY_HIP(h, hipMemsetAsync(h->d_dist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
   AIY_HIP(h, hipMemsetAsync(h->d_last, 0, sizeof(int) * n_cal, st));
   const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
   int next = 1;
@@ -276,13 +283,13 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
     }
     AIY_CHECK_LAUNCH(h);
     AIY_HIP(h, hipMemcpyAsync(h->h_last, h->d_last, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
-    AIY_HIP(h, hipMemcpyAsync(h->h_dist, h->d_dist, sizeof(unsigned long long) * 3 * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipMemcpyAsync(h->h_dist, h->d_dist, sizeof(unsigned long long) * kSlots * n_cal, hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipStreamSynchronize(st));
     bool all = true;
     for (int c = 0; c < n_cal; ++c) {
       const int last = h->h_last[c];
       double d;
-      unsigned long long bits = h->h_dist[c * 3 + last % 3];
+      unsigned long long bits = h->h_dist[c * kSlots + last % 3];
       memcpy(&d, &bits, sizeof(d));
       const bool conv = (last >= 2 && !(d > tol)) || last >= last_allowed;
       all = all && conv;
@@ -292,7 +299,7 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   }
   for (int c = 0; c < n_cal; ++c) {
     const int last = h->h_last[c];
-    unsigned long long bits = h->h_dist[c * 3 + last % 3];
+    unsigned long long bits = h->h_dist[c * kSlots + last % 3];
     double d;
     memcpy(&d, &bits, sizeof(d));
     cycles_out[c] = last;

@@ -20,6 +20,8 @@
 
 namespace aiy {
 
+constexpr int kSlots = 4;  // per-calibration convergence words (3 distance slots + flag)
+
 __device__ __forceinline__ int upper_bound(const double* __restrict__ x, int lo, int hi, double q) {
   while (lo < hi) {
     int mid = lo + ((hi - lo) >> 1);
@@ -84,8 +86,9 @@ __global__ __launch_bounds__(256) void hist_push_kernel(int S, int n_a, const in
                                                         const double* __restrict__ mass, double* __restrict__ T,
                                                         const unsigned long long* dslots, int iter, double tol) {
   const int cal = blockIdx.z, s = blockIdx.y;
-  if (dslots && iter >= 2) {
-    const double dprev = __longlong_as_double((long long)dslots[cal * 3 + (iter - 1) % 3]);
+  if (dslots && iter >= 2) {   // same sticky protocol as the EGM solve (egm.hip)
+    if (load_u64_agent(&dslots[cal * kSlots + 3]) != 0ull) return;
+    const double dprev = __longlong_as_double((long long)load_u64_agent(&dslots[cal * kSlots + (iter - 1) % 3]));
     if (!(dprev >= tol)) return;
   }
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,9 +110,13 @@ __global__ __launch_bounds__(256) void hist_mix_kernel(int S, int n_a, const dou
                                                        double* __restrict__ mass_out, unsigned long long* dslots,
                                                        int* last_iter, int iter, double tol) {
   const int cal = blockIdx.y;
-  if (dslots && iter >= 2) {
-    const double dprev = __longlong_as_double((long long)dslots[cal * 3 + (iter - 1) % 3]);
-    if (!(dprev >= tol)) return;
+  if (dslots && iter >= 2) {   // same sticky protocol as the EGM solve (egm.hip)
+    if (load_u64_agent(&dslots[cal * kSlots + 3]) != 0ull) return;
+    const double dprev = __longlong_as_double((long long)load_u64_agent(&dslots[cal * kSlots + (iter - 1) % 3]));
+    if (!(dprev >= tol)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) store_u64_agent(&dslots[cal * kSlots + 3], 1ull);
+      return;
+    }
   }
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = j < n_a;
@@ -144,9 +151,9 @@ __global__ __launch_bounds__(256) void hist_mix_kernel(int S, int n_a, const dou
     if (threadIdx.x == 0) {
       double d = red[0];
       for (int w2 = 1; w2 < (int)(blockDim.x / kWave); ++w2) d = nan_max(d, red[w2]);
-      atomicMax(&dslots[cal * 3 + iter % 3], (unsigned long long)__double_as_longlong(d));
+      atomicMax(&dslots[cal * kSlots + iter % 3], (unsigned long long)__double_as_longlong(d));
       if (blockIdx.x == 0) {
-        dslots[cal * 3 + (iter + 1) % 3] = 0ull;
+        store_u64_agent(&dslots[cal * kSlots + (iter + 1) % 3], 0ull);
         last_iter[cal] = iter;
       }
     }
@@ -176,10 +183,10 @@ static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
   if (h->h_hdist) { (void)hipHostFree(h->h_hdist); (void)hipHostFree(h->h_K); (void)hipHostFree(h->h_hlast); }
   h->d_hdist = nullptr; h->d_K = nullptr; h->d_hlast = nullptr;
   h->h_hdist = nullptr; h->h_K = nullptr; h->h_hlast = nullptr; h->hist_cap = 0;
-  AIY_HIP(h, hipMalloc((void**)&h->d_hdist, sizeof(unsigned long long) * 3 * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_hdist, sizeof(unsigned long long) * kSlots * n_cal));
   AIY_HIP(h, hipMalloc((void**)&h->d_K, sizeof(double) * n_cal));
   AIY_HIP(h, hipMalloc((void**)&h->d_hlast, sizeof(int) * n_cal));
-  AIY_HIP(h, hipHostMalloc((void**)&h->h_hdist, sizeof(unsigned long long) * 3 * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_hdist, sizeof(unsigned long long) * kSlots * n_cal, hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_K, sizeof(double) * n_cal, hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_hlast, sizeof(int) * n_cal, hipHostMallocDefault));
   h->hist_cap = n_cal;
@@ -221,7 +228,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
   double* T = work;          // [n_cal][S][n_a] push accumulator (kept zero between iterations)
   double* alt = work + per;  // [n_cal][S][n_a] ping-pong partner of `mass`
   AIY_HIP(h, hipMemsetAsync(T, 0, per * sizeof(double), st));
-  AIY_HIP(h, hipMemsetAsync(h->d_hdist, 0, sizeof(unsigned long long) * 3 * n_cal, st));
+  AIY_HIP(h, hipMemsetAsync(h->d_hdist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
   AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * n_cal, st));
   dim3 gpush((n_a + 255) / 256, S, n_cal);
   dim3 gmix((n_a + 255) / 256, n_cal);
@@ -243,13 +250,13 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
     }
     AIY_CHECK_LAUNCH(h);
     AIY_HIP(h, hipMemcpyAsync(h->h_hlast, h->d_hlast, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
-    AIY_HIP(h, hipMemcpyAsync(h->h_hdist, h->d_hdist, sizeof(unsigned long long) * 3 * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipMemcpyAsync(h->h_hdist, h->d_hdist, sizeof(unsigned long long) * kSlots * n_cal, hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipStreamSynchronize(st));
     bool all = true;
     for (int c = 0; c < n_cal; ++c) {
       const int last = h->h_hlast[c];
       double d;
-      unsigned long long b = h->h_hdist[c * 3 + last % 3];
+      unsigned long long b = h->h_hdist[c * kSlots + last % 3];
       std::memcpy(&d, &b, sizeof(d));
       all = all && ((last >= 1 && !(d >= tol)) || last >= max_iter);
     }

@@ -37,10 +37,10 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, long 
                                                                const double* __restrict__ u, unsigned long long seed,
                                                                unsigned ctr0, const double* __restrict__ sow,
                                                                double* __restrict__ partials) {
-  const double Mnow = sow[0];
-  const int Mrkv = (int)sow[2];
-  const double Rnow = sow[3];
-  const double Wnow = sow[4];
+  const double Mnow = load_f64_agent(&sow[0]);
+  const int Mrkv = (int)load_f64_agent(&sow[2]);
+  const double Rnow = load_f64_agent(&sow[3]);
+  const double Wnow = load_f64_agent(&sow[4]);
   const int n_M = P.n_M, n1 = P.n_a + 1, n_lab = P.n_lab;
   // LinearInterpOnInterp1D bracket in M: the same for every agent of the period.
   int j = 1;
@@ -96,14 +96,14 @@ __global__ __launch_bounds__(256) void period_sum_kernel(const double* __restric
   for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, kWave);
   if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
   __syncthreads();
-  if (threadIdx.x == 0) sow[6] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) store_f64_agent(&sow[6], (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 // calc_R_and_W (AS:1839-1894) from the (all-reduced) sum in sow[6].
 __global__ void period_price_kernel(aiy_market mk, const int* __restrict__ mrkv_hist, long long n_total, int t,
                                     double* sow, double* hist_A, double* hist_M) {
   if (threadIdx.x != 0) return;
-  const double Aprev = sow[6] / (double)n_total;   // np.mean(np.array(aNow))
+  const double Aprev = load_f64_agent(&sow[6]) / (double)n_total;   // np.mean(np.array(aNow))
   const double AggK = Aprev;
   const int Mrkv = mrkv_hist[t];
   const double Prod = mk.prod[Mrkv ? 1 : 0];
@@ -113,12 +113,12 @@ __global__ void period_price_kernel(aiy_market mk, const int* __restrict__ mrkv_
   const double Rnow = 1.0 + Prod * (al * pow(KtoL, al - 1.0)) - mk.depr_fac;
   const double Wnow = Prod * ((1.0 - al) * pow(KtoL, al));
   const double Mnow = Rnow * AggK + Wnow * AggL;
-  sow[0] = Mnow;
-  sow[1] = Aprev;
-  sow[2] = (double)Mrkv;
-  sow[3] = Rnow;
-  sow[4] = Wnow;
-  sow[5] = 0.0;  // Urate: everyone employed at UrateB = UrateG = 0
+  store_f64_agent(&sow[0], Mnow);
+  store_f64_agent(&sow[1], Aprev);
+  store_f64_agent(&sow[2], (double)Mrkv);
+  store_f64_agent(&sow[3], Rnow);
+  store_f64_agent(&sow[4], Wnow);
+  store_f64_agent(&sow[5], 0.0);  // Urate: everyone employed at UrateB = UrateG = 0
   if (hist_A) hist_A[t] = Aprev;
   if (hist_M) hist_M[t] = Mnow;
 }

@@ -18,7 +18,7 @@ F64 = torch.float64
 
 
 def _dev(x, device) -> torch.Tensor:
-    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), dtype=F64).to(device).contiguous()
+    return torch.from_numpy(np.array(x, dtype=np.float64, order="C", copy=True)).to(device)
 
 
 @dataclass
