@@ -24,6 +24,7 @@ ERRORS = {-1: "AIY_ERR_ARG", -2: "AIY_ERR_HIP", -3: "AIY_ERR_STATE", -4: "AIY_ER
           -5: "AIY_ERR_COMM"}
 AIY_MAX_STATES = 64
 AIY_SOW_DOUBLES = 8
+AIY_OPT_USE_GRAPHS = 1
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -47,7 +48,7 @@ class Market(ctypes.Structure):
 class PanelModel(ctypes.Structure):
     _fields_ = [("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32), ("n_lab", ctypes.c_int32),
                 ("m_pol", vp), ("c_pol", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
-                ("mrkv_hist", vp)]
+                ("mrkv_hist", vp), ("pol_index", vp)]
 
 
 # name -> (restype, argtypes)
@@ -59,11 +60,19 @@ SIGNATURES = {
     "aiy_egm_step": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), vp, vp, vp, vp, vp]),
     "aiy_egm_solve": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, c_int32_p, c_double_p, vp]),
+    "aiy_egm_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), vp, vp, vp, vp,
+                                             ctypes.c_int32, ctypes.POINTER(ctypes.c_float), vp]),
     "aiy_policy_eval": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp,
                                          ctypes.c_int64, vp, vp]),
     "aiy_sim_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]),
+    "aiy_sim_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
+                                             vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_float), vp]),
+    "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
+    "aiy_index_ints_per_row": (ctypes.c_int32, []),
+    "aiy_build_index": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]),
     "aiy_comm_unique_id": (ctypes.c_int32, [vp]),
     "aiy_comm_init": (ctypes.c_int32, [vp, vp, ctypes.c_int32, ctypes.c_int32]),
     "aiy_comm_destroy": (ctypes.c_int32, [vp]),

@@ -29,9 +29,12 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->d_dist) (void)hipFree(h->d_dist);
   if (h->d_last) (void)hipFree(h->d_last);
+  if (h->d_egm_idx) (void)hipFree(h->d_egm_idx);
   if (h->h_dist) (void)hipHostFree(h->h_dist);
   if (h->h_last) (void)hipHostFree(h->h_last);
   if (h->d_partials) (void)hipFree(h->d_partials);
+  if (h->d_ticket) (void)hipFree(h->d_ticket);
+  if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
   if (h->d_hdist) (void)hipFree(h->d_hdist);
   if (h->d_K) (void)hipFree(h->d_K);
   if (h->d_hlast) (void)hipFree(h->d_hlast);

@@ -112,6 +112,50 @@ __device__ __forceinline__ double interp_row(const double* __restrict__ x, const
 }
 
 // ---------------------------------------------------------------------------------
+// Log-bucket search index of a sorted, positive row x[0..n) (the m nodes of one
+// LinearInterp, searched over x[:-1]).  Bucket b covers the doubles whose bit
+// pattern >> kIdxShift equals base + b, base = key(x[1]) (x[0] is the 1e-7 borrowing
+// node, far below the rest of the row): kIdxPerOctave buckets per binary octave.
+// H[b] = first i with x[i] >= edge_b = lower_bound(x, edge_b).  A query in bucket b has
+// its lower_bound in [H[b], H[b+1]] (queries below edge_0: [0, H[0]]; above the last
+// bucket: [H[K], n]), found exactly -- bucket edges are bit-level, no floating-point
+// rounding -- by a search over a handful of nodes.
+//   layout per row: H[0 .. kIdxBuckets] (kIdxBuckets + 1 ints), base at [kIdxBuckets + 1]
+// ---------------------------------------------------------------------------------
+constexpr int kIdxShift = 44;                   // 8 mantissa bits -> 256 buckets / octave
+constexpr int kIdxBuckets = 16 * 256;           // 16 octaves above x[1]
+constexpr int kIdxRow = kIdxBuckets + 2;        // ints per row
+constexpr int kIdxNoBase = -2147483647 - 1;     // x[1] <= 0 or n < 2: index unusable -> full search
+
+__device__ __forceinline__ long long idx_key(double q) {
+  return (long long)(__double_as_longlong(q) >> kIdxShift);
+}
+
+// lower_bound(x[0..n), q) using the row index H (nullptr -> plain binary search).
+__device__ __forceinline__ int locate(const double* __restrict__ x, int n, const int* __restrict__ H, double q) {
+  int lo = 0, hi = n;
+  if (H != nullptr) {
+    const int base = H[kIdxBuckets + 1];
+    if (base != kIdxNoBase) {
+      const long long key = idx_key(q) - (long long)base;
+      if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
+      else if (key >= kIdxBuckets) { lo = H[kIdxBuckets]; hi = n; }
+      else { lo = H[key]; hi = H[key + 1]; }
+      if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }   // defensive: unsorted rows
+    }
+  }
+  return lower_bound(x, lo, hi, q);
+}
+
+// HARK LinearInterp of one row through the index.
+__device__ __forceinline__ double interp_row_idx(const double* __restrict__ x, const double* __restrict__ y, int n,
+                                                 const int* __restrict__ H, double q) {
+  int i = locate(x, n, H, q);
+  i = i < 1 ? 1 : i;
+  return lerp_at(x, y, i, q, x[0]);
+}
+
+// ---------------------------------------------------------------------------------
 // x ** -gam and x ** (-1/gam) with NumPy's fast scalar-power path for gam == 1
 // (ndarray ** -1.0 is np.reciprocal).  kind: 1 -> gam == 1; 0 -> generic pow.
 // ---------------------------------------------------------------------------------

@@ -45,6 +45,85 @@ struct EgmDev {
   const double* crra;
 };
 
+// Phase 1 + 2 of one EGM point (cal, k, i) for all S current states.  LOG selects
+// MargValueFuncCRRA/inversion with CRRA == 1 (NumPy's reciprocal fast path) at compile
+// time: with a runtime select the compiler evaluated the f64 pow unconditionally
+// (measured: 25k VALU instructions per wave, 1 ms per cycle at N_a = 10 000).
+template <int SMAX, bool TERMINAL, bool LOG>
+__device__ __forceinline__ double egm_point(const EgmDev& A, const double* __restrict__ m_next,
+                                            const double* __restrict__ c_next, double* __restrict__ m_out,
+                                            double* __restrict__ c_out, const int* __restrict__ idx_next, int cal,
+                                            int k, int i, bool active, bool track, double* Vs) {
+  const int S = A.S, n_M = A.n_M, n_a = A.n_a, n1 = n_a + 1;
+  const double a = A.a_grid[(size_t)cal * n_a + (active ? i : n_a - 1)];
+  const double gam = A.crra[cal];
+  const double beta = A.beta[cal];
+  const double* Rk = A.R_next + ((size_t)cal * n_M + k) * S;
+  const double* Wk = A.W_next + ((size_t)cal * n_M + k) * S;
+  const double* Mk = A.M_next + ((size_t)cal * n_M + k) * S;
+  const double* lab = A.lab + (size_t)cal * S;
+  const double* Mg = A.M_grid + (size_t)cal * n_M;
+  const size_t tab_cal = (size_t)cal * S * n_M * n1;
+
+  // Phase 1 (runtime loop over s'): V[s'] = R * vP_{s'}(m', M') staged in LDS, one
+  // column per lane (conflict-free), so the unrolled contraction below can pull the
+  // whole vector into registers with compile-time indices.
+  for (int sp = 0; sp < S; ++sp) {
+    const double R = Rk[sp];
+    const double q = R * a + Wk[sp] * lab[sp];  // mNextArray (AS:1024)
+    double c;
+    if constexpr (TERMINAL) {
+      c = q * 1.0;  // IdentityFunction (AS:898)
+    } else {
+      const double* bm = m_next + tab_cal + (size_t)sp * n_M * n1;
+      const double* bc = c_next + tab_cal + (size_t)sp * n_M * n1;
+      const int* H0 = idx_next ? idx_next + ((size_t)cal * S + sp) * n_M * kIdxRow : nullptr;
+      if (n_M == 1) {
+        c = interp_row_idx(bm, bc, n_a, H0, q);
+      } else {
+        // LinearInterpOnInterp1D: y_pos = clip(searchsorted(Mgrid, M'), 1, n_M - 1)
+        const double Mp = Mk[sp];
+        int j = lower_bound(Mg, 0, n_M, Mp);
+        j = j > n_M - 1 ? n_M - 1 : j;
+        j = j < 1 ? 1 : j;
+        const double alpha = (Mp - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
+        const double f0 = interp_row_idx(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, n_a,
+                                         H0 ? H0 + (size_t)(j - 1) * kIdxRow : nullptr, q);
+        const double f1 = interp_row_idx(bm + (size_t)j * n1, bc + (size_t)j * n1, n_a,
+                                         H0 ? H0 + (size_t)j * kIdxRow : nullptr, q);
+        c = (1 - alpha) * f0 + alpha * f1;
+      }
+    }
+    const double vP = LOG ? 1.0 / c : pow(c, -gam);  // MargValueFuncCRRA
+    Vs[sp * kEgmBlock + threadIdx.x] = R * vP;       // RnextArray * vPnext
+  }
+  double V[SMAX];
+#pragma unroll
+  for (int sp = 0; sp < SMAX; ++sp) V[sp] = (sp < S) ? Vs[sp * kEgmBlock + threadIdx.x] : 0.0;
+
+  // Phase 2: E[s] = beta * sum_s' V[s'] P[s, s'] (NumPy pairwise order), invert, write.
+  const double* Pc = A.P + (size_t)cal * S * S;
+  double dmax = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double* Ps = Pc + (size_t)s * S;
+    const double sum = np_pairwise_sum<SMAX>(S, [&](int t) { return V[t] * Ps[t]; });
+    const double E = beta * sum;                              // EndOfPrdvP (AS:1485)
+    const double c = LOG ? 1.0 / E : pow(E, -1.0 / gam);      // AS:1490
+    const double m = a + c;                                   // AS:1499
+    const size_t row = tab_cal + ((size_t)s * n_M + k) * n1;
+    if (active) {
+      m_out[row + i + 1] = m;
+      c_out[row + i + 1] = c;
+      if (track) dmax = nan_max(dmax, nan_max(fabs(m - m_next[row + i + 1]), fabs(c - c_next[row + i + 1])));
+    }
+    if (i == 0) {
+      m_out[row] = kBorrowNode;
+      c_out[row] = kBorrowNode;
+    }
+  }
+  return dmax;
+}
+
 // Convergence protocol (solve mode, dist_slots != nullptr), per calibration 4 words:
 // three rotating distance slots and a sticky "converged" flag.  Cycle n returns at
 // once if the flag is set or if cycle n-1 met !(d > tol) (HARK: go = distance >
@@ -55,7 +134,8 @@ template <int SMAX, bool TERMINAL>
 __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const double* __restrict__ m_next,
                                                               const double* __restrict__ c_next,
                                                               double* __restrict__ m_out,
-                                                              double* __restrict__ c_out, int cycle,
+                                                              double* __restrict__ c_out,
+                                                              const int* __restrict__ idx_next, int cycle,
                                                               unsigned long long* dist_slots,
                                                               int* last_cycle, double tol) {
   const int cal = blockIdx.z;
@@ -69,74 +149,15 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
       return;
     }
   }
-  const int S = A.S, n_M = A.n_M, n_a = A.n_a, n1 = n_a + 1;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n_a;
-  const double a = A.a_grid[(size_t)cal * n_a + (active ? i : n_a - 1)];
-  const double gam = A.crra[cal];
-  const double beta = A.beta[cal];
-  const bool log_util = (gam == 1.0);  // NumPy fast path: x ** -1.0 is np.reciprocal
-  const double* Rk = A.R_next + ((size_t)cal * n_M + k) * S;
-  const double* Wk = A.W_next + ((size_t)cal * n_M + k) * S;
-  const double* Mk = A.M_next + ((size_t)cal * n_M + k) * S;
-  const double* lab = A.lab + (size_t)cal * S;
-  const double* Mg = A.M_grid + (size_t)cal * n_M;
-  const size_t tab_cal = (size_t)cal * S * n_M * n1;
-
-  // Phase 1 (runtime loop over s'): V[s'] = R * vP_{s'}(m', M') staged in LDS, one
-  // column per lane (conflict-free), so the unrolled contraction below can pull the
-  // whole vector into registers with compile-time indices.
-  __shared__ double Vs[SMAX * kEgmBlock];
-  for (int sp = 0; sp < S; ++sp) {
-    const double R = Rk[sp];
-    const double q = R * a + Wk[sp] * lab[sp];  // mNextArray (AS:1024)
-    double c;
-    if constexpr (TERMINAL) {
-      c = q * 1.0;  // IdentityFunction (AS:898)
-    } else {
-      const double* bm = m_next + tab_cal + (size_t)sp * n_M * n1;
-      const double* bc = c_next + tab_cal + (size_t)sp * n_M * n1;
-      if (n_M == 1) {
-        c = interp_row_wave(bm, bc, n_a, q, active);
-      } else {
-        // LinearInterpOnInterp1D: y_pos = clip(searchsorted(Mgrid, M'), 1, n_M - 1)
-        const double Mp = Mk[sp];
-        int j = lower_bound(Mg, 0, n_M, Mp);
-        j = j > n_M - 1 ? n_M - 1 : j;
-        j = j < 1 ? 1 : j;
-        const double alpha = (Mp - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
-        const double f0 = interp_row_wave(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, n_a, q, active);
-        const double f1 = interp_row_wave(bm + (size_t)j * n1, bc + (size_t)j * n1, n_a, q, active);
-        c = (1 - alpha) * f0 + alpha * f1;
-      }
-    }
-    const double vP = log_util ? 1.0 / c : pow(c, -gam);  // MargValueFuncCRRA
-    Vs[sp * kEgmBlock + threadIdx.x] = R * vP;             // RnextArray * vPnext
-  }
-  double V[SMAX];
-#pragma unroll
-  for (int sp = 0; sp < SMAX; ++sp) V[sp] = (sp < S) ? Vs[sp * kEgmBlock + threadIdx.x] : 0.0;
-
-  const double* Pc = A.P + (size_t)cal * S * S;
-  double dmax = 0.0;
+  const bool active = i < A.n_a;
   const bool track = (dist_slots != nullptr) && cycle >= 2;
-  for (int s = 0; s < S; ++s) {
-    const double* Ps = Pc + (size_t)s * S;
-    const double sum = np_pairwise_sum<SMAX>(S, [&](int t) { return V[t] * Ps[t]; });
-    const double E = beta * sum;                                   // EndOfPrdvP (AS:1485)
-    const double c = log_util ? 1.0 / E : pow(E, -1.0 / gam);      // AS:1490
-    const double m = a + c;                                        // AS:1499
-    const size_t row = tab_cal + ((size_t)s * n_M + k) * n1;
-    if (active) {
-      m_out[row + i + 1] = m;
-      c_out[row + i + 1] = c;
-      if (track) dmax = nan_max(dmax, nan_max(fabs(m - m_next[row + i + 1]), fabs(c - c_next[row + i + 1])));
-    }
-    if (i == 0) {
-      m_out[row] = kBorrowNode;
-      c_out[row] = kBorrowNode;
-    }
-  }
+  __shared__ double Vs[SMAX * kEgmBlock];
+  double dmax;
+  if (A.crra[cal] == 1.0)   // block-uniform: one of two straight-line bodies
+    dmax = egm_point<SMAX, TERMINAL, true>(A, m_next, c_next, m_out, c_out, idx_next, cal, k, i, active, track, Vs);
+  else
+    dmax = egm_point<SMAX, TERMINAL, false>(A, m_next, c_next, m_out, c_out, idx_next, cal, k, i, active, track, Vs);
 
   if (dist_slots != nullptr) {
     if (track) {
@@ -204,23 +225,33 @@ static EgmDev to_dev(const aiy_egm_dims* d, const aiy_egm_inputs* in) {
 
 template <bool TERM>
 static void launch_cycle_t(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co,
-                           int cycle, unsigned long long* ds, int* lc, double tol, hipStream_t st) {
+                           const int* ix, int cycle, unsigned long long* ds, int* lc, double tol, hipStream_t st) {
   dim3 grid((A.n_a + kEgmBlock - 1) / kEgmBlock, A.n_M, A.n_cal);
   dim3 block(kEgmBlock);
   if (A.S <= 8)
-    hipLaunchKernelGGL((egm_cycle_kernel<8, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+    hipLaunchKernelGGL((egm_cycle_kernel<8, TERM>), grid, block, 0, st, A, mn, cn, mo, co, ix, cycle, ds, lc, tol);
   else if (A.S <= 16)
-    hipLaunchKernelGGL((egm_cycle_kernel<16, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+    hipLaunchKernelGGL((egm_cycle_kernel<16, TERM>), grid, block, 0, st, A, mn, cn, mo, co, ix, cycle, ds, lc, tol);
   else if (A.S <= 32)
-    hipLaunchKernelGGL((egm_cycle_kernel<32, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+    hipLaunchKernelGGL((egm_cycle_kernel<32, TERM>), grid, block, 0, st, A, mn, cn, mo, co, ix, cycle, ds, lc, tol);
   else
-    hipLaunchKernelGGL((egm_cycle_kernel<64, TERM>), grid, block, 0, st, A, mn, cn, mo, co, cycle, ds, lc, tol);
+    hipLaunchKernelGGL((egm_cycle_kernel<64, TERM>), grid, block, 0, st, A, mn, cn, mo, co, ix, cycle, ds, lc, tol);
 }
 
-static void launch_cycle(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co, int cycle,
-                         unsigned long long* ds, int* lc, double tol, hipStream_t st) {
-  if (mn == nullptr) launch_cycle_t<true>(A, mn, cn, mo, co, cycle, ds, lc, tol, st);
-  else launch_cycle_t<false>(A, mn, cn, mo, co, cycle, ds, lc, tol, st);
+static void launch_cycle(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co, const int* ix,
+                         int cycle, unsigned long long* ds, int* lc, double tol, hipStream_t st) {
+  if (mn == nullptr) launch_cycle_t<true>(A, mn, cn, mo, co, nullptr, cycle, ds, lc, tol, st);
+  else launch_cycle_t<false>(A, mn, cn, mo, co, ix, cycle, ds, lc, tol, st);
+}
+
+static int32_t ensure_egm_index(aiy_handle* h, size_t ints) {
+  if (ints <= h->egm_idx_cap) return AIY_OK;
+  if (h->d_egm_idx) (void)hipFree(h->d_egm_idx);
+  h->d_egm_idx = nullptr;
+  h->egm_idx_cap = 0;
+  AIY_HIP(h, hipMalloc((void**)&h->d_egm_idx, ints * sizeof(int)));
+  h->egm_idx_cap = ints;
+  return AIY_OK;
 }
 
 static int32_t ensure_egm_scratch(aiy_handle* h, int n_cal) {
@@ -249,7 +280,17 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
   if (!m_out || !c_out) return fail(h, AIY_ERR_ARG, "null output");
   AIY_HIP(h, hipSetDevice(h->device));
   EgmDev A = to_dev(dims, in);
-  launch_cycle(A, m_next, c_next, m_out, c_out, 0, nullptr, nullptr, 0.0, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  const long long rows = (long long)dims->n_cal * dims->S * dims->n_M;
+  const int* ix = nullptr;
+  if (m_next) {
+    rc = ensure_egm_index(h, (size_t)rows * kIdxRow);
+    if (rc) return rc;
+    rc = launch_build_index(h, m_next, rows, dims->n_a + 1, h->d_egm_idx, st);
+    if (rc) return rc;
+    ix = h->d_egm_idx;
+  }
+  launch_cycle(A, m_next, c_next, m_out, c_out, ix, 0, nullptr, nullptr, 0.0, st);
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
 }
@@ -270,6 +311,10 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   const size_t per_cal = (size_t)dims->S * dims->n_M * (dims->n_a + 1);
   const size_t buf = per_cal * n_cal;
   EgmDev A = to_dev(dims, in);
+  const long long rows = (long long)n_cal * dims->S * dims->n_M;
+  const size_t idx_per = (size_t)rows * kIdxRow;
+  rc = ensure_egm_index(h, 2 * idx_per);
+  if (rc) return rc;
   AIY_HIP(h, hipMemsetAsync(h->d_dist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
   AIY_HIP(h, hipMemsetAsync(h->d_last, 0, sizeof(int) * n_cal, st));
   const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
@@ -279,7 +324,11 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
     for (int cyc = next; cyc < end; ++cyc) {
       const double* mn = cyc == 1 ? nullptr : work_m + ((cyc - 1) & 1) * buf;
       const double* cn = cyc == 1 ? nullptr : work_c + ((cyc - 1) & 1) * buf;
-      launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, cyc, h->d_dist, h->d_last, tol, st);
+      const int* ix = cyc == 1 ? nullptr : h->d_egm_idx + ((cyc - 1) & 1) * idx_per;
+      launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, ix, cyc, h->d_dist, h->d_last, tol,
+                   st);
+      rc = launch_build_index(h, work_m + (cyc & 1) * buf, rows, dims->n_a + 1, h->d_egm_idx + (cyc & 1) * idx_per, st);
+      if (rc) return rc;
     }
     AIY_CHECK_LAUNCH(h);
     AIY_HIP(h, hipMemcpyAsync(h->h_last, h->d_last, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
@@ -327,6 +376,37 @@ extern "C" int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_
   const long long nb = (n + tb - 1) / tb;
   hipLaunchKernelGGL(policy_eval_kernel, dim3((unsigned)nb), dim3(tb), 0, as_stream(stream), S, n_M, n_a, m_tab,
                      c_tab, M_grid, state, m, M, (long long)n, c_out);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
+// Timing hook for bench.py: n_launch launches of the EGM cycle kernel alone (the search
+// index of m_next is built once, outside the timed region) between two HIP events on
+// `stream`.  BLOCKING.
+extern "C" int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
+                                       const double* m_next, const double* c_next, double* m_out, double* c_out,
+                                       int32_t n_launch, float* ms_out, aiy_stream stream) {
+  int32_t rc = check_egm(h, dims, in);
+  if (rc) return rc;
+  if (!m_next || !c_next || !m_out || !c_out || !ms_out || n_launch < 1) return fail(h, AIY_ERR_ARG, "bad arguments");
+  AIY_HIP(h, hipSetDevice(h->device));
+  EgmDev A = to_dev(dims, in);
+  hipStream_t st = as_stream(stream);
+  const long long rows = (long long)dims->n_cal * dims->S * dims->n_M;
+  rc = ensure_egm_index(h, (size_t)rows * kIdxRow);
+  if (rc) return rc;
+  rc = launch_build_index(h, m_next, rows, dims->n_a + 1, h->d_egm_idx, st);
+  if (rc) return rc;
+  hipEvent_t e0, e1;
+  AIY_HIP(h, hipEventCreate(&e0));
+  AIY_HIP(h, hipEventCreate(&e1));
+  AIY_HIP(h, hipEventRecord(e0, st));
+  for (int k = 0; k < n_launch; ++k) launch_cycle(A, m_next, c_next, m_out, c_out, h->d_egm_idx, 0, nullptr, nullptr, 0.0, st);
+  AIY_HIP(h, hipEventRecord(e1, st));
+  AIY_HIP(h, hipEventSynchronize(e1));
+  AIY_HIP(h, hipEventElapsedTime(ms_out, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
 }

@@ -18,12 +18,17 @@ struct aiy_handle {
   unsigned long long* d_dist = nullptr;
   int* d_last = nullptr;
   size_t egm_cap = 0;
+  int* d_egm_idx = nullptr;          // [2][rows][kIdxRow] search index of the ping-pong tables
+  size_t egm_idx_cap = 0;            // ints
   // host pinned mirrors
   unsigned long long* h_dist = nullptr;
   int* h_last = nullptr;
   // panel: per-block partial sums
   double* d_partials = nullptr;
+  unsigned* d_ticket = nullptr;      // last-block-done counter of the period kernel
   size_t partials_cap = 0;
+  hipStream_t cap_stream = nullptr;  // hipGraph capture stream
+  bool use_graphs = true;
   // histogram: per-calibration sup-norm slots [n_cal][3] + sums of K
   unsigned long long* d_hdist = nullptr;
   double* d_K = nullptr;
@@ -38,6 +43,8 @@ struct aiy_handle {
 };
 
 namespace aiy {
+
+int32_t launch_build_index(aiy_handle* h, const double* x, long long n_rows, int n1, int* H, hipStream_t st);
 
 inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
   char buf[512];

@@ -1,17 +1,21 @@
 // Monte Carlo panel for gfx950.
 //
-// One period of Market.make_history ([HARK] sow -> cultivate -> reap -> mill) becomes
-//   sim_period_kernel    every agent: labour draw (np.random.choice inverse CDF,
-//                        Aiyagari_Support.py:1253-1254), m = R a + W l
-//                        (AS:1283), c = cFunc[4l + 2 Mrkv + emp](m, M) (AS:1326-1408),
-//                        a = m - c (AS:1415); per-block partial sums of a;
-//   period_sum_kernel    fixed-order sum of the block partials (deterministic);
-//   [ncclAllReduce]      when agents are sharded over ranks;
-//   period_price_kernel  calc_R_and_W (AS:1867-1894): K = mean a, prices, history.
-// The market state ("sow_state") never leaves the device; the host only enqueues.
-// Agents are processed one per lane with a grid-stride loop whose grid depends only on
-// the local agent count, so the summation order -- and hence every bit of the
-// history -- is independent of the device and of timing.
+// One period of Market.make_history ([HARK] sow -> cultivate -> reap -> mill) is ONE
+// kernel launch on a single GPU:
+//   every agent (one per lane, grid-stride): labour draw (np.random.choice inverse CDF,
+//   Aiyagari_Support.py:1253-1254), m = R a + W l (AS:1283),
+//   c = cFunc[4 l + 2 Mrkv + emp](m, M) (AS:1326-1408), a = m - c (AS:1415);
+//   per-block partial sum of a -> the LAST block to arrive (write-through partials +
+//   agent-scope ticket, cdna_hip_programming.md Guideline 16) sums the partials in
+//   fixed order and runs mill/calc_R_and_W (AS:1867-1894), writing the next sow_state
+//   and the history.
+// The period index lives on the device (sow[7]) so every launch of a history has
+// identical arguments: aiy_sim_periods captures a block of periods into a hipGraph
+// once and replays it, which takes the host out of the per-period loop.
+// With agents sharded over ranks the last block only publishes the
+// local sum; an ncclAllReduce and a 1-thread price kernel follow on the same stream.
+// The grid depends only on the local agent count and the partial sums are combined in
+// fixed order, so every bit of the history is reproducible run to run.
 #include "common.h"
 #include "internal.h"
 
@@ -21,6 +25,7 @@ namespace aiy {
 
 constexpr int kSimBlock = 256;
 constexpr int kSimMaxBlocks = 8192;
+constexpr int kGraphPeriods = 64;
 
 struct PanelDev {
   int S, n_M, n_a, n_lab;
@@ -30,80 +35,31 @@ struct PanelDev {
   const double* lab_level;
   const double* lab_cdf;
   const int* mrkv_hist;
+  const int* pol_index;
 };
 
-__global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, long long n, long long offset,
-                                                               double* __restrict__ a, uint8_t* __restrict__ lab,
-                                                               const double* __restrict__ u, unsigned long long seed,
-                                                               unsigned ctr0, const double* __restrict__ sow,
-                                                               double* __restrict__ partials) {
-  const double Mnow = load_f64_agent(&sow[0]);
-  const int Mrkv = (int)load_f64_agent(&sow[2]);
-  const double Rnow = load_f64_agent(&sow[3]);
-  const double Wnow = load_f64_agent(&sow[4]);
-  const int n_M = P.n_M, n1 = P.n_a + 1, n_lab = P.n_lab;
-  // LinearInterpOnInterp1D bracket in M: the same for every agent of the period.
-  int j = 1;
-  double alpha = 0.0;
-  if (n_M > 1) {
-    j = lower_bound(P.M_grid, 0, n_M, Mnow);
-    j = j > n_M - 1 ? n_M - 1 : j;
-    j = j < 1 ? 1 : j;
-    alpha = (Mnow - P.M_grid[j - 1]) / (P.M_grid[j] - P.M_grid[j - 1]);
-  }
-  double local = 0.0;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += stride) {
-    const int lp = lab[idx];
-    const double uu = u ? u[idx] : philox_uniform(ctr0, (uint64_t)(offset + idx), seed, 0u);
-    const double* cdf = P.lab_cdf + (size_t)lp * n_lab;
-    int ln = 0;
-    for (int t = 0; t < n_lab; ++t) ln += (cdf[t] <= uu) ? 1 : 0;  // searchsorted(cdf, u, 'right')
-    const double m = Rnow * a[idx] + Wnow * (P.lab_level[ln] * 1.0);
-    const int s = 4 * ln + 2 * Mrkv + 1;                                // employed (Urate = 0)
-    const double* bm = P.m_pol + (size_t)s * n_M * n1;
-    const double* bc = P.c_pol + (size_t)s * n_M * n1;
-    double c;
-    if (n_M == 1) {
-      c = interp_row(bm, bc, P.n_a, m);
-    } else {
-      const double f0 = interp_row(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, P.n_a, m);
-      const double f1 = interp_row(bm + (size_t)j * n1, bc + (size_t)j * n1, P.n_a, m);
-      c = (1 - alpha) * f0 + alpha * f1;
-    }
-    const double an = m - c;
-    a[idx] = an;
-    lab[idx] = (uint8_t)ln;
-    local += an;
-  }
-  __shared__ double red[kSimBlock / kWave];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = local;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = red[0];
-    for (int w = 1; w < kSimBlock / kWave; ++w) s += red[w];
-    partials[blockIdx.x] = s;
-  }
-}
+struct PanelRun {
+  long long n, offset, n_total;
+  double* a;
+  uint8_t* lab;
+  const double* u;   // uniforms [.. ][u_ld] starting at period u_t0, or nullptr (Philox)
+  long long u_ld;
+  int u_t0;
+  unsigned long long seed;
+  unsigned ge_iter;
+  double* sow;
+  double* partials;
+  unsigned* ticket;
+  double* hist_A;
+  double* hist_M;
+  int finish;        // 1: last block computes prices (single rank); 0: publish local sum only
+};
 
-__global__ __launch_bounds__(256) void period_sum_kernel(const double* __restrict__ partials, int nb, double* sow) {
-  double s = 0.0;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += partials[b];
-  __shared__ double red[256 / kWave];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) store_f64_agent(&sow[6], (red[0] + red[1]) + (red[2] + red[3]));
-}
-
-// calc_R_and_W (AS:1839-1894) from the (all-reduced) sum in sow[6].
-__global__ void period_price_kernel(aiy_market mk, const int* __restrict__ mrkv_hist, long long n_total, int t,
-                                    double* sow, double* hist_A, double* hist_M) {
-  if (threadIdx.x != 0) return;
-  const double Aprev = load_f64_agent(&sow[6]) / (double)n_total;   // np.mean(np.array(aNow))
+// calc_R_and_W (AS:1839-1894) given the sum of end-of-period assets over all agents.
+__device__ __forceinline__ void mill(const aiy_market& mk, const int* mrkv_hist, long long n_total, double sum_a,
+                                     double* sow, double* hist_A, double* hist_M) {
+  const int t = (int)load_f64_agent(&sow[7]);
+  const double Aprev = sum_a / (double)n_total;   // np.mean(np.array(aNow))
   const double AggK = Aprev;
   const int Mrkv = mrkv_hist[t];
   const double Prod = mk.prod[Mrkv ? 1 : 0];
@@ -119,13 +75,198 @@ __global__ void period_price_kernel(aiy_market mk, const int* __restrict__ mrkv_
   store_f64_agent(&sow[3], Rnow);
   store_f64_agent(&sow[4], Wnow);
   store_f64_agent(&sow[5], 0.0);  // Urate: everyone employed at UrateB = UrateG = 0
+  store_f64_agent(&sow[7], (double)(t + 1));
   if (hist_A) hist_A[t] = Aprev;
   if (hist_M) hist_M[t] = Mnow;
+}
+
+// Two LinearInterp bracket searches (rows j-1 and j of one state) advanced in
+// lock-step so their dependent loads overlap; each starts from its index window.
+__device__ __forceinline__ void locate2(const double* __restrict__ x0, const double* __restrict__ x1, int& lo0,
+                                        int hi0, int& lo1, int hi1, double q) {
+  while (lo0 < hi0 || lo1 < hi1) {
+    const int m0 = lo0 + ((hi0 - lo0) >> 1);
+    const int m1 = lo1 + ((hi1 - lo1) >> 1);
+    const bool a0 = lo0 < hi0, a1 = lo1 < hi1;
+    const double v0 = a0 ? x0[m0] : 0.0;
+    const double v1 = a1 ? x1[m1] : 0.0;
+    if (a0) { if (v0 < q) lo0 = m0 + 1; else hi0 = m0; }
+    if (a1) { if (v1 < q) lo1 = m1 + 1; else hi1 = m1; }
+  }
+}
+
+__device__ __forceinline__ void index_window(const int* __restrict__ H, int base, int n, double q, int& lo, int& hi) {
+  lo = 0;
+  hi = n;
+  if (H == nullptr || base == kIdxNoBase) return;
+  const long long key = idx_key(q) - (long long)base;
+  if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
+  else if (key >= kIdxBuckets) { lo = H[kIdxBuckets]; hi = n; }
+  else { lo = H[key]; hi = H[key + 1]; }
+  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
+}
+
+constexpr int kLdsLab = 16;   // labour chains up to 16 states are staged in LDS
+
+__global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, PanelRun r, aiy_market mk) {
+  const double Mnow = load_f64_agent(&r.sow[0]);
+  const int Mrkv = (int)load_f64_agent(&r.sow[2]);
+  const double Rnow = load_f64_agent(&r.sow[3]);
+  const double Wnow = load_f64_agent(&r.sow[4]);
+  const int t = (int)load_f64_agent(&r.sow[7]);
+  const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
+  const double* u = r.u ? r.u + (size_t)(t - r.u_t0) * r.u_ld : nullptr;
+  const int n_M = P.n_M, n_a = P.n_a, n1 = n_a + 1, n_lab = P.n_lab;
+  // LinearInterpOnInterp1D bracket in M: the same for every agent of the period.
+  int j = 1;
+  double alpha = 0.0;
+  if (n_M > 1) {
+    j = lower_bound(P.M_grid, 0, n_M, Mnow);
+    j = j > n_M - 1 ? n_M - 1 : j;
+    j = j < 1 ? 1 : j;
+    alpha = (Mnow - P.M_grid[j - 1]) / (P.M_grid[j] - P.M_grid[j - 1]);
+  }
+  const int jlo = n_M > 1 ? j - 1 : 0;
+  const int jhi = n_M > 1 ? j : 0;
+  // Stage the labour chain (inverse CDF rows, levels) and the index bases of this
+  // period's rows in LDS: the per-agent dependent chain then has one global hop less.
+  __shared__ double s_cdf[kLdsLab * kLdsLab];
+  __shared__ double s_lvl[kLdsLab];
+  __shared__ int s_base[2 * kLdsLab];
+  const bool lds_lab = n_lab <= kLdsLab;
+  if (lds_lab) {
+    for (int q = threadIdx.x; q < n_lab * n_lab; q += blockDim.x) s_cdf[q] = P.lab_cdf[q];
+    for (int q = threadIdx.x; q < n_lab; q += blockDim.x) {
+      s_lvl[q] = P.lab_level[q];
+      const int s = 4 * q + 2 * Mrkv + 1;
+      s_base[2 * q] = P.pol_index ? P.pol_index[((size_t)s * n_M + jlo) * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
+      s_base[2 * q + 1] = P.pol_index ? P.pol_index[((size_t)s * n_M + jhi) * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
+    }
+  }
+  __syncthreads();
+  double local = 0.0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < r.n; idx += stride) {
+    const int lp = r.lab[idx];
+    const double a_prev = r.a[idx];
+    const double uu = u ? u[idx] : philox_uniform(ctr0, (uint64_t)(r.offset + idx), r.seed, 0u);
+    int ln = 0;
+    if (lds_lab) {
+      for (int q = 0; q < n_lab; ++q) ln += (s_cdf[lp * n_lab + q] <= uu) ? 1 : 0;  // searchsorted(cdf, u, 'right')
+    } else {
+      const double* cdf = P.lab_cdf + (size_t)lp * n_lab;
+      for (int q = 0; q < n_lab; ++q) ln += (cdf[q] <= uu) ? 1 : 0;
+    }
+    const double lvl = lds_lab ? s_lvl[ln] : P.lab_level[ln];
+    const double m = Rnow * a_prev + Wnow * (lvl * 1.0);                 // AS:1283
+    const int s = 4 * ln + 2 * Mrkv + 1;                                 // employed (Urate = 0)
+    const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
+    const double* x0 = P.m_pol + r0 * n1;
+    const double* x1 = P.m_pol + r1 * n1;
+    int b0, b1;
+    if (lds_lab) { b0 = s_base[2 * ln]; b1 = s_base[2 * ln + 1]; }
+    else {
+      b0 = P.pol_index ? P.pol_index[r0 * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
+      b1 = P.pol_index ? P.pol_index[r1 * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
+    }
+    int lo0, hi0, lo1, hi1;
+    index_window(P.pol_index ? P.pol_index + r0 * kIdxRow : nullptr, b0, n_a, m, lo0, hi0);
+    index_window(P.pol_index ? P.pol_index + r1 * kIdxRow : nullptr, b1, n_a, m, lo1, hi1);
+    locate2(x0, x1, lo0, hi0, lo1, hi1, m);
+    const int i0 = lo0 < 1 ? 1 : lo0;
+    const int i1 = lo1 < 1 ? 1 : lo1;
+    const double f0 = lerp_at(x0, P.c_pol + r0 * n1, i0, m, x0[0]);
+    double c = f0;
+    if (n_M > 1) {
+      const double f1 = lerp_at(x1, P.c_pol + r1 * n1, i1, m, x1[0]);
+      c = (1 - alpha) * f0 + alpha * f1;                                 // LinearInterpOnInterp1D
+    }
+    const double an = m - c;                                             // AS:1415
+    r.a[idx] = an;
+    r.lab[idx] = (uint8_t)ln;
+    local += an;
+  }
+  // ---- block partial, then the last block finishes the period ----
+  __shared__ double red[kSimBlock / kWave];
+  __shared__ int is_last;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // Hand-off without fences (MI355X_MICROARCH.md, "Valid forms", row 1): the partial is
+    // stored write-through (sc1), drained, then counted with an agent-scope atomic; the
+    // last arriver reads every partial with sc1 loads.  A per-block release fence here
+    // would write back the XCD's whole L2 (the dirty a/lab lines) once per block.
+    const double s = (red[0] + red[1]) + (red[2] + red[3]);
+    store_f64_agent(&r.partials[blockIdx.x], s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(r.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == gridDim.x - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) acc += load_f64_agent(&r.partials[b]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
+  __syncthreads();
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double total = (red[0] + red[1]) + (red[2] + red[3]);
+    __hip_atomic_store(r.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r.finish) mill(mk, P.mrkv_hist, r.n_total, total, r.sow, r.hist_A, r.hist_M);
+    else store_f64_agent(&r.sow[6], total);
+  }
+}
+
+// Sharded path: prices from the all-reduced sum in sow[6].
+__global__ void period_price_kernel(aiy_market mk, const int* __restrict__ mrkv_hist, long long n_total, double* sow,
+                                    double* hist_A, double* hist_M) {
+  if (threadIdx.x != 0) return;
+  mill(mk, mrkv_hist, n_total, load_f64_agent(&sow[6]), sow, hist_A, hist_M);
+}
+
+// No local agents on this rank (sharded path only): publish a zero sum.
+__global__ void zero_sum_kernel(double* sow) {
+  if (threadIdx.x == 0) store_f64_agent(&sow[6], 0.0);
+}
+
+__global__ void set_period_kernel(double* sow, int t) {
+  if (threadIdx.x == 0) store_f64_agent(&sow[7], (double)t);
 }
 
 static int sim_blocks(long long n) {
   long long nb = (n + kSimBlock - 1) / kSimBlock;
   return (int)std::max(1LL, std::min<long long>(nb, kSimMaxBlocks));
+}
+
+static int32_t ensure_panel_scratch(aiy_handle* h) {
+  if (h->partials_cap >= (size_t)kSimMaxBlocks) return AIY_OK;
+  AIY_HIP(h, hipMalloc((void**)&h->d_partials, sizeof(double) * kSimMaxBlocks));
+  AIY_HIP(h, hipMalloc((void**)&h->d_ticket, sizeof(unsigned)));
+  AIY_HIP(h, hipMemset(h->d_ticket, 0, sizeof(unsigned)));
+  AIY_HIP(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+  h->partials_cap = kSimMaxBlocks;
+  return AIY_OK;
+}
+
+// Enqueue one period (1 launch single-rank; 3 launches + 1 collective when sharded).
+static int32_t enqueue_period(aiy_handle* h, const PanelDev& P, const PanelRun& r, const aiy_market& mk, int nb,
+                              hipStream_t st) {
+  if (r.n > 0) {
+    hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, r, mk);
+  } else {
+    hipLaunchKernelGGL(zero_sum_kernel, dim3(1), dim3(64), 0, st, r.sow);
+  }
+  if (!r.finish) {
+    ncclResult_t e = ncclAllReduce(r.sow + 6, r.sow + 6, 1, ncclDouble, ncclSum, h->comm, st);
+    if (e != ncclSuccess) return fail(h, AIY_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(e));
+    hipLaunchKernelGGL(period_price_kernel, dim3(1), dim3(64), 0, st, mk, P.mrkv_hist, r.n_total, r.sow, r.hist_A,
+                       r.hist_M);
+  }
+  return AIY_OK;
 }
 
 }  // namespace aiy
@@ -150,38 +291,101 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   if (u && u_ld < n_local) return fail(h, AIY_ERR_ARG, "u_ld < n_local");
   if (t0 < 0 || n_periods < 0 || t0 + (int64_t)n_periods > (1 << 20)) return fail(h, AIY_ERR_ARG, "bad period range");
   if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
+  if (!h->comm && n_local != n_total) return fail(h, AIY_ERR_ARG, "n_local != n_total without a communicator");
   if (n_periods == 0) return AIY_OK;
   AIY_HIP(h, hipSetDevice(h->device));
+  int32_t rc = ensure_panel_scratch(h);
+  if (rc) return rc;
   hipStream_t st = as_stream(stream);
   const int nb = sim_blocks(n_local);
-  if ((size_t)nb > h->partials_cap) {
-    if (h->d_partials) (void)hipFree(h->d_partials);
-    h->d_partials = nullptr;
-    AIY_HIP(h, hipMalloc((void**)&h->d_partials, sizeof(double) * kSimMaxBlocks));
-    h->partials_cap = kSimMaxBlocks;
-  }
   PanelDev P;
   P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
   P.m_pol = model->m_pol; P.c_pol = model->c_pol; P.M_grid = model->M_grid;
   P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
-  for (int p = 0; p < n_periods; ++p) {
-    const int t = t0 + p;
-    const unsigned ctr0 = (ge_iter << 20) | (unsigned)t;
-    const double* up = u ? u + (size_t)p * u_ld : nullptr;
-    if (n_local > 0) {
-      hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, (long long)n_local,
-                         (long long)agent_offset, a, lab, up, (unsigned long long)seed, ctr0, sow, h->d_partials);
-      hipLaunchKernelGGL(period_sum_kernel, dim3(1), dim3(256), 0, st, h->d_partials, nb, sow);
-    } else {
-      AIY_HIP(h, hipMemsetAsync(sow + 6, 0, sizeof(double), st));
+  P.pol_index = model->pol_index;
+  PanelRun r;
+  r.n = n_local; r.offset = agent_offset; r.n_total = n_total; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld;
+  r.u_t0 = t0; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.hist_A = hist_A; r.hist_M = hist_M; r.finish = h->comm ? 0 : 1;
+  const aiy_market mk = *mkt;
+
+  hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
+  int done = 0;
+  if (h->use_graphs && !h->comm && n_periods >= 2 * kGraphPeriods) {
+    // Capture kGraphPeriods identical periods on the handle's capture stream, replay.
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    AIY_HIP(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+    for (int p = 0; p < kGraphPeriods; ++p) {
+      rc = enqueue_period(h, P, r, mk, nb, h->cap_stream);
+      if (rc) {
+        hipGraph_t junk;
+        (void)hipStreamEndCapture(h->cap_stream, &junk);
+        return rc;
+      }
     }
-    if (h->comm) {
-      ncclResult_t r = ncclAllReduce(sow + 6, sow + 6, 1, ncclDouble, ncclSum, h->comm, st);
-      if (r != ncclSuccess) return fail(h, AIY_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-    }
-    hipLaunchKernelGGL(period_price_kernel, dim3(1), dim3(64), 0, st, *mkt, model->mrkv_hist, (long long)n_total, t,
-                       sow, hist_A, hist_M);
+    AIY_HIP(h, hipStreamEndCapture(h->cap_stream, &g));
+    AIY_HIP(h, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    const int reps = n_periods / kGraphPeriods;
+    for (int k = 0; k < reps; ++k) AIY_HIP(h, hipGraphLaunch(ge, st));
+    done = reps * kGraphPeriods;
+    // the executable graph is released only after its replays ran: this call blocks
+    AIY_HIP(h, hipStreamSynchronize(st));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+  }
+  for (int p = done; p < n_periods; ++p) {
+    rc = enqueue_period(h, P, r, mk, nb, st);
+    if (rc) return rc;
   }
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
+}
+
+// Timing hook for bench.py: n_launch back-to-back launches of the per-period kernel
+// alone (agent update + block partials + last-block mill) between two HIP events on
+// `stream`; returns the elapsed milliseconds.  Advances the panel state like
+// n_launch periods of a history.
+extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
+                                       int64_t n_local, double* a, uint8_t* lab, uint64_t seed, uint32_t ge_iter,
+                                       double* sow, int32_t n_launch, float* ms_out, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (!model || !mkt || !sow || !a || !lab || !ms_out || n_local < 1 || n_launch < 1)
+    return fail(h, AIY_ERR_ARG, "bad arguments");
+  AIY_HIP(h, hipSetDevice(h->device));
+  int32_t rc = ensure_panel_scratch(h);
+  if (rc) return rc;
+  hipStream_t st = as_stream(stream);
+  PanelDev P;
+  P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
+  P.m_pol = model->m_pol; P.c_pol = model->c_pol; P.M_grid = model->M_grid;
+  P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
+  P.pol_index = model->pol_index;
+  PanelRun r;
+  r.n = n_local; r.offset = 0; r.n_total = n_local; r.a = a; r.lab = lab; r.u = nullptr; r.u_ld = 0; r.u_t0 = 0;
+  r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 1;
+  const int nb = sim_blocks(n_local);
+  hipEvent_t e0, e1;
+  AIY_HIP(h, hipEventCreate(&e0));
+  AIY_HIP(h, hipEventCreate(&e1));
+  hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, 0);
+  AIY_HIP(h, hipEventRecord(e0, st));
+  for (int k = 0; k < n_launch; ++k)
+    hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, r, *mkt);
+  AIY_HIP(h, hipEventRecord(e1, st));
+  AIY_HIP(h, hipEventSynchronize(e1));
+  AIY_HIP(h, hipEventElapsedTime(ms_out, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) {
+  if (!h) return AIY_ERR_ARG;
+  switch (option) {
+    case AIY_OPT_USE_GRAPHS: h->use_graphs = value != 0; return AIY_OK;
+    default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
+  }
 }

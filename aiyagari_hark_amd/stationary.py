@@ -1,0 +1,172 @@
+"""Stationary Aiyagari extensions (build-defined, no reference code).
+
+``solve_table2`` solves many calibrations to general equilibrium at once:
+
+  bisection on r (E1)  -- per calibration, all brackets advanced together
+    w(r) = (1 - alpha) (alpha / (r + delta))^(alpha / (1 - alpha)),  R = 1 + r
+    stationary EGM  -- aiy_egm_solve with one aggregate node (n_M = 1): the reference's
+                       solve_Aiyagari arithmetic (Aiyagari_Support.py:1478-1504) with
+                       constant prices, batched over calibrations
+    Young lottery   -- aiy_hist_lottery + aiy_hist_solve (E2): stationary distribution
+                       on the asset grid, K_s(r) = sum mass * a
+    K_d(r) = (alpha / (r + delta))^(1 / (1 - alpha)); move the bracket toward K_s = K_d.
+
+Income processes: the reference's Tauchen (Aiyagari_Support.py:885-887, 7 states) or
+Rouwenhorst (E3, e.g. 25 states for the stress configuration), levels normalised by
+their simple mean (quirk Q3).  Everything per grid point runs in libaiyagari; the
+host only moves the brackets.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import setup_math as sm
+from .egm import EgmBatch, egm_solve
+
+F64 = torch.float64
+
+# Aiyagari (1994) Table II grid: rho x sigma x mu
+TABLE2_RHO = (0.0, 0.3, 0.6, 0.9)
+TABLE2_SIGMA = (0.2, 0.4)
+TABLE2_CRRA = (1.0, 3.0, 5.0)
+
+
+@dataclass
+class Calibration:
+    LaborAR: float = 0.6
+    LaborSD: float = 0.2
+    CRRA: float = 1.0
+    DiscFac: float = 0.96
+    CapShare: float = 0.36
+    DeprFac: float = 0.08
+    LaborStatesNo: int = 7
+    income: str = "tauchen"       # or "rouwenhorst"
+
+    def income_process(self):
+        if self.income == "tauchen":
+            y, P = sm.labor_tauchen(self.LaborStatesNo, self.LaborAR, self.LaborSD)
+        elif self.income == "rouwenhorst":
+            y, P = sm.rouwenhorst(self.LaborStatesNo, self.LaborAR, self.LaborSD)
+        else:
+            raise ValueError(self.income)
+        return sm.labor_levels(y), P
+
+
+def table2_calibrations(**kw):
+    """The 24 calibrations of Aiyagari (1994) Table II (rho, sigma, CRRA)."""
+    return [Calibration(LaborAR=r, LaborSD=s, CRRA=c, **kw)
+            for s in TABLE2_SIGMA for r in TABLE2_RHO for c in TABLE2_CRRA]
+
+
+def firm_prices(r, alpha, delta):
+    """(w, K_demand) with L = 1 (Cobb-Douglas firm of calc_R_and_W, AS:1886-1890)."""
+    KtoL = (alpha / (r + delta)) ** (1.0 / (1.0 - alpha))
+    return (1.0 - alpha) * KtoL ** alpha, KtoL
+
+
+@dataclass
+class StationaryResult:
+    r: np.ndarray
+    K: np.ndarray
+    K_supply: np.ndarray
+    KtoY: np.ndarray
+    saving_rate: np.ndarray
+    bisection_steps: int
+    egm_cycles: list = field(default_factory=list)
+    hist_iters: list = field(default_factory=list)
+
+
+class StationaryBatch:
+    """Device buffers for one batch of stationary calibrations on a common grid size."""
+
+    def __init__(self, cals, aGrid, device=None):
+        self.cals = list(cals)
+        self.device = torch.device(device or "cuda")
+        n_cal = len(self.cals)
+        levels, Ps = zip(*(c.income_process() for c in self.cals))
+        S = len(levels[0])
+        if any(len(l) != S for l in levels):
+            raise ValueError("all calibrations of a batch need the same number of income states")
+        self.S = S
+        self.n_a = int(np.asarray(aGrid).shape[-1])
+        self.aGrid = np.broadcast_to(np.asarray(aGrid, dtype=np.float64), (n_cal, self.n_a)).copy()
+        self.levels = np.stack(levels)
+        self.P = np.stack(Ps)
+        dev = self.device
+        self.d_a = torch.as_tensor(self.aGrid).to(dev)
+        self.d_P = torch.as_tensor(self.P).to(dev)
+        self.d_lab = torch.as_tensor(self.levels).to(dev)
+        self.d_beta = torch.as_tensor([c.DiscFac for c in self.cals], dtype=F64).to(dev)
+        self.d_crra = torch.as_tensor([c.CRRA for c in self.cals], dtype=F64).to(dev)
+        self.alpha = np.array([c.CapShare for c in self.cals])
+        self.delta = np.array([c.DeprFac for c in self.cals])
+        shp = (n_cal, S, self.n_a)
+        self.lo = torch.empty(shp, dtype=torch.int32, device=dev)
+        self.wlo = torch.empty(shp, dtype=F64, device=dev)
+        self.mass = torch.empty(shp, dtype=F64, device=dev)
+        self.work = torch.empty((2,) + shp, dtype=F64, device=dev)
+
+    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000):
+        """K_s(r) for every calibration (r: array [n_cal])."""
+        n_cal, S = len(self.cals), self.S
+        r = np.asarray(r, dtype=np.float64)
+        w, _ = firm_prices(r, self.alpha, self.delta)
+        R = 1.0 + r
+        dev = self.device
+        Rn = torch.as_tensor(np.repeat(R[:, None, None], S, axis=2)).to(dev)
+        Wn = torch.as_tensor(np.repeat(w[:, None, None], S, axis=2)).to(dev)
+        batch = EgmBatch(self.d_a, torch.zeros((n_cal, 1), dtype=F64, device=dev), self.d_P, Rn, Wn,
+                         torch.zeros_like(Rn), self.d_lab, self.d_beta, self.d_crra)
+        m, c, cycles, _ = egm_solve(batch, tol=egm_tol)
+        h = _lib.handle(dev.index)
+        dR = torch.as_tensor(R).to(dev)
+        dw = torch.as_tensor(w).to(dev)
+        sp = _lib.stream_ptr()
+        h.check(h.lib.aiy_hist_lottery(h.h, n_cal, S, self.n_a, _lib.ptr(m), _lib.ptr(c), _lib.ptr(self.d_a),
+                                       _lib.ptr(dR), _lib.ptr(dw), _lib.ptr(self.d_lab), _lib.ptr(self.lo),
+                                       _lib.ptr(self.wlo), sp), "aiy_hist_lottery")
+        self.mass.fill_(1.0 / (S * self.n_a))
+        K = (ctypes.c_double * n_cal)()
+        iters = (ctypes.c_int32 * n_cal)()
+        h.check(h.lib.aiy_hist_solve(h.h, n_cal, S, self.n_a, _lib.ptr(self.lo), _lib.ptr(self.wlo),
+                                     _lib.ptr(self.d_P), _lib.ptr(self.d_a), float(hist_tol), int(max_hist), 64,
+                                     _lib.ptr(self.mass), _lib.ptr(self.work), K, iters, sp), "aiy_hist_solve")
+        self.last_tables = (m, c)
+        return np.array(K[:]), np.array(cycles), np.array(iters[:])
+
+
+def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
+                 hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None):
+    """GE bisection on r (E1) for every calibration at once.  Returns StationaryResult."""
+    cals = table2_calibrations() if cals is None else list(cals)
+    aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
+    b = StationaryBatch(cals, aGrid, device=device)
+    n = len(cals)
+    lo = np.full(n, -0.5 * b.delta) if r_lo is None else np.broadcast_to(np.asarray(r_lo, float), (n,)).copy()
+    hi = (1.0 / np.array([c.DiscFac for c in cals]) - 1.0 - 1e-9) if r_hi is None else \
+        np.broadcast_to(np.asarray(r_hi, float), (n,)).copy()
+    steps = 0
+    cyc_log, it_log = [], []
+    Ks = np.zeros(n)
+    while np.any(hi - lo > r_tol) and steps < max_steps:
+        mid = 0.5 * (lo + hi)
+        Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol)
+        _, Kd = firm_prices(mid, b.alpha, b.delta)
+        up = Ks > Kd
+        hi = np.where(up, mid, hi)
+        lo = np.where(up, lo, mid)
+        steps += 1
+        cyc_log.append(cycles)
+        it_log.append(iters)
+        if log is not None:
+            log.append(dict(step=steps, r=mid.copy(), Ks=Ks.copy(), Kd=Kd.copy()))
+    r = 0.5 * (lo + hi)
+    _, K = firm_prices(r, b.alpha, b.delta)
+    KtoY = K ** (1.0 - b.alpha)
+    return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
+                            egm_cycles=cyc_log, hist_iters=it_log)

@@ -97,12 +97,28 @@ int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inp
                       double* m_out, double* c_out, int32_t* cycles_out, double* dist_out,
                       aiy_stream stream);
 
+/* Measurement hook (bench.py): n_launch launches of the EGM cycle kernel alone from
+ * (m_next, c_next) (search index built once, outside the timed region), bracketed by
+ * HIP events on `stream`; *ms_out = elapsed milliseconds.  BLOCKING. */
+int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
+                            const double* m_next, const double* c_next, double* m_out, double* c_out,
+                            int32_t n_launch, float* ms_out, aiy_stream stream);
+
 /* cFunc[state](m, M) for a batch of queries (interop for .solution[0].cFunc and the
  * notebook's plots, AH:271-275): HARK LinearInterpOnInterp1D semantics.
  *   tables [S][n_M][n_a+1]; state/m/M [n]; c_out [n].  Asynchronous. */
 int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_t n_a, const double* m_tab,
                         const double* c_tab, const double* M_grid, const int32_t* state,
                         const double* m, const double* M, int64_t n, double* c_out, aiy_stream stream);
+
+/* Search index of policy rows (accelerates every HARK LinearInterp bracket search
+ * without changing its result): for each of n_rows rows x[0..n1) (the m nodes of one
+ * LinearInterp, x[0] > 0, sorted) build a log-bucket table of
+ * aiy_index_ints_per_row() int32 so that lower_bound(x[:-1], q) is found by a search
+ * over a few nodes.  Asynchronous. */
+int32_t aiy_index_ints_per_row(void);
+int32_t aiy_build_index(aiy_handle* h, int64_t n_rows, int32_t n1, const double* x, int32_t* index,
+                        aiy_stream stream);
 
 /* ----------------------------- panel (rows B1-B6, C2) ----------------------------- */
 
@@ -123,10 +139,12 @@ typedef struct {
   const double* lab_level; /* [n_lab] LSStates (AS:1265)                                  */
   const double* lab_cdf;   /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
   const int32_t* mrkv_hist;/* [act_T] MrkvNow_hist (AS:1793-1805)                          */
+  const int32_t* pol_index;/* [S][n_M][aiy_index_ints_per_row()] from aiy_build_index(m_pol),
+                              or NULL (plain binary search)                                 */
 } aiy_panel_model;
 
 /* Device-resident market state ("sow_state", AS:1585), 8 doubles:
- *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] local sum(a) [7] reserved */
+ *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] sum(a) [7] period index t */
 #define AIY_SOW_DOUBLES 8
 
 /* Simulate periods t0 .. t0 + n_periods - 1 of Market.make_history (AH:249 ->
@@ -134,18 +152,33 @@ typedef struct {
  * local agent (get_shocks AS:1217-1256, get_states AS:1259-1283, get_controls
  * AS:1286-1409, get_poststates AS:1411-1415), then mill/calc_R_and_W (AS:1839-1894)
  * on the mean of `a` over all n_total agents of all ranks, writing sow and
- * hist_A[t] = Aprev, hist_M[t] = Mnow (the track_vars of AS:1587).
+ * hist_A[t] = Aprev, hist_M[t] = Mnow (the track_vars of AS:1587).  sow[7] holds the
+ * period index on device.
  *   a [n_local] (in: a_prev, out: a_now), lab [n_local] uint8 labour state
  *   u: NULL -> on-device Philox4x32-10 (counter (ge_iter<<20 | t, idx, 0), key seed),
- *      else host-supplied uniforms [n_periods][u_ld] (parity with np.random.choice)
+ *      else host-supplied uniforms [n_periods][u_ld] starting at period t0 (parity
+ *      with np.random.choice)
  *   agent_offset: global index of local agent 0 (Philox counter, sharding)
  * With a communicator bound (aiy_comm_init) the per-period sum of a is all-reduced
- * over RCCL before the prices are formed.  Asynchronous. */
+ * over RCCL before the prices are formed; otherwise n_local must equal n_total.
+ * Asynchronous, except that with hipGraph replay enabled (default; single rank,
+ * n_periods >= 128) the call returns after the replayed periods completed. */
 int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                         int64_t n_local, int64_t agent_offset, int64_t n_total, double* a,
                         uint8_t* lab, const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter,
                         int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
                         aiy_stream stream);
+
+/* Measurement hook (bench.py): n_launch back-to-back launches of the per-period panel
+ * kernel (single rank, Philox shocks) bracketed by HIP events recorded on `stream`;
+ * *ms_out = elapsed milliseconds.  Advances a/lab/sow like n_launch periods.  BLOCKING. */
+int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
+                            int64_t n_local, double* a, uint8_t* lab, uint64_t seed, uint32_t ge_iter,
+                            double* sow, int32_t n_launch, float* ms_out, aiy_stream stream);
+
+/* Handle options. */
+#define AIY_OPT_USE_GRAPHS 1 /* value != 0: replay panel periods from a captured hipGraph */
+int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
 /* 128-byte ncclUniqueId created by rank 0 and broadcast by the host. */

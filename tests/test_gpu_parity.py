@@ -201,3 +201,72 @@ def test_ge_fixed_point_matches_oracle(gpu):
     # cFunc interop (Aiyagari-HARK.py:275)
     xi = agent.solution[0].cFunc[0].xInterpolators
     assert len(xi) == 15 and xi[0].x_list.shape == (33,)
+
+
+def test_search_index_equals_binary_search(gpu):
+    """aiy_build_index + indexed lookup return exactly numpy searchsorted's bracket:
+    evaluated through policy_eval-free path by comparing one EGM step with/without index."""
+    from aiyagari_hark_amd import _lib
+    fx = np.load(os.path.join(GOLD, "egm_cfg1_afunc2.npz"))
+    h = _lib.handle(0)
+    ipr = h.lib.aiy_index_ints_per_row()
+    m = torch.as_tensor(fx["m"]).to(gpu).reshape(-1, fx["m"].shape[-1]).contiguous()
+    idx = torch.empty((m.shape[0], ipr), dtype=torch.int32, device=gpu)
+    h.check(h.lib.aiy_build_index(h.h, m.shape[0], m.shape[1], _lib.ptr(m), _lib.ptr(idx), _lib.stream_ptr()), "idx")
+    torch.cuda.synchronize()
+    H = idx.cpu().numpy()
+    x = fx["m"].reshape(-1, fx["m"].shape[-1])
+    shift = 44
+    for r in range(0, x.shape[0], 37):
+        xr = x[r, :-1]
+        base = int(H[r, -1])
+        assert base == int(np.float64(x[r, 1]).view(np.int64) >> shift)
+        for b in range(0, ipr - 1, 97):
+            edge = np.int64((base + b) << shift).view(np.float64)
+            assert H[r, b] == np.searchsorted(xr, edge), (r, b)
+
+
+def test_stationary_capital_supply_matches_oracle(gpu):
+    """E1/E2 at r = 4 %: stationary EGM tables bit-exact (CRRA 1), Young-lottery K to 1e-10."""
+    from aiyagari_hark_amd.stationary import Calibration, StationaryBatch
+    fx = np.load(os.path.join(GOLD, "stationary.npz"))
+    b = StationaryBatch([Calibration()], fx["aGrid"], device=gpu)
+    K, cycles, iters = b.capital_supply(np.array([float(fx["r"])]), egm_tol=1e-8, hist_tol=1e-12)
+    m, c = b.last_tables
+    assert int(cycles[0]) == int(fx["cycles"])
+    assert rel_err(c[0, :, 0].cpu().numpy(), fx["c"]) == 0.0
+    assert abs(K[0] - float(fx["K"])) / float(fx["K"]) < 1e-10
+    assert abs(int(iters[0]) - int(fx["hist_iters"])) <= 2
+    mass = b.mass[0].cpu().numpy()
+    assert abs(mass.sum() - 1.0) < 1e-12
+    assert np.max(np.abs(mass - fx["mass"])) < 1e-12
+
+
+def test_stationary_bisection_matches_oracle(gpu):
+    """GE bisection on r for a 3-calibration batch (mixed CRRA, Rouwenhorst row) vs the oracle."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    from oracle import stationary as ST
+    cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=3.0),
+            Calibration(LaborAR=0.3, LaborSD=0.2, CRRA=5.0)]
+    res = solve_table2(cals, n_a=120, r_tol=1e-6, device=gpu)
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 120, 2)
+    for k, cal in enumerate(cals):
+        lab, P = ST.income_process(7, cal.LaborAR, cal.LaborSD, "tauchen")
+        want = ST.ge_bisect(dict(DiscFac=0.96, CRRA=cal.CRRA, CapShare=0.36, DeprFac=0.08), aGrid, lab, P,
+                            r_tol=1e-6)
+        assert abs(res.r[k] - want["r"]) < 1e-5
+        assert abs(res.KtoY[k] - want["KtoY"]) < 1e-5
+
+
+def test_rouwenhorst_25_state_histogram(gpu):
+    """Stress shape (25-state Rouwenhorst, S = 25 > 16): K_s(r) vs oracle."""
+    from aiyagari_hark_amd.stationary import Calibration, StationaryBatch
+    from oracle import stationary as ST
+    cal = Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0, LaborStatesNo=25, income="rouwenhorst")
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 300, 2)
+    b = StationaryBatch([cal], aGrid, device=gpu)
+    K, cycles, iters = b.capital_supply(np.array([0.02]), egm_tol=1e-8, hist_tol=1e-12)
+    lab, P = ST.income_process(25, 0.9, 0.4, "rouwenhorst")
+    Kw, info = ST.capital_supply(0.02, dict(DiscFac=0.96, CRRA=5.0, CapShare=0.36, DeprFac=0.08), aGrid, lab, P)
+    assert int(cycles[0]) == info["cycles"]
+    assert abs(K[0] - Kw) / Kw < 1e-9
