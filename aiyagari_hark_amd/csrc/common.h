@@ -118,9 +118,10 @@ __device__ __forceinline__ double interp_row(const double* __restrict__ x, const
 // node, far below the rest of the row): kIdxPerOctave buckets per binary octave.
 // H[b] = first i with x[i] >= edge_b = lower_bound(x, edge_b).  A query in bucket b has
 // its lower_bound in [H[b], H[b+1]] (queries below edge_0: [0, H[0]]; above the last
-// bucket: [H[K], n]), found exactly -- bucket edges are bit-level, no floating-point
+// node's bucket: n), found exactly -- bucket edges are bit-level, no floating-point
 // rounding -- by a search over a handful of nodes.
-//   layout per row: H[0 .. kIdxBuckets] (kIdxBuckets + 1 ints), base at [kIdxBuckets + 1]
+//   layout per row: H[0 .. kIdxBuckets - 1] buckets (entries up to last + 1 valid),
+//   last = bucket of the last node at [kIdxBuckets], base at [kIdxBuckets + 1]
 // ---------------------------------------------------------------------------------
 constexpr int kIdxShift = 44;                   // 8 mantissa bits -> 256 buckets / octave
 constexpr int kIdxBuckets = 16 * 256;           // 16 octaves above x[1]
@@ -138,8 +139,12 @@ __device__ __forceinline__ int locate(const double* __restrict__ x, int n, const
     const int base = H[kIdxBuckets + 1];
     if (base != kIdxNoBase) {
       const long long key = idx_key(q) - (long long)base;
+      const int last = H[kIdxBuckets];
       if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-      else if (key >= kIdxBuckets) { lo = H[kIdxBuckets]; hi = n; }
+      else if (key >= kIdxBuckets - 1) {                    // capped top bucket / beyond the span
+        if (last == kIdxBuckets - 1) { lo = H[kIdxBuckets - 1]; hi = n; } else { lo = n; hi = n; }
+      }
+      else if (key > last) { lo = n; hi = n; }              // above every node
       else { lo = H[key]; hi = H[key + 1]; }
       if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }   // defensive: unsorted rows
     }

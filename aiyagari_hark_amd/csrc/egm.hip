@@ -5,21 +5,24 @@
 // reference's 4-D NumPy tiling):
 //   * the reference tiles mNext/Mnext/R/P to [a, M, s, s'] (precompute_arrays,
 //     Aiyagari_Support.py:906-1037) and evaluates every next-period marginal value 28x
-//     (once per current state s).  Here a thread owns one (calibration, M node k,
-//     asset node i) and evaluates V[s'] = R[k,s'] * c_{s'}(m'(i,k,s'), M'[k,s'])^-rho
-//     ONCE per s', keeping all S values in registers;
-//   * the expectation E[s] = beta * sum_{s'} V[s'] P[s,s'] (AS:1485) is then an S x S
-//     register contraction per thread, summed in NumPy's pairwise order, with P read
-//     through the scalar cache (block-uniform addresses);
-//   * next-period consumption c_{s'}(m, M') is HARK's LinearInterpOnInterp1D over the
-//     two M rows that bracket M' (block-uniform), each a LinearInterp whose bracket is
-//     found by a wave-cooperative monotone search: queries m'(i) = R a_i + W l are
-//     increasing in i, so the wave finds [lb(q_min), lb(q_max)] with two wave-uniform
-//     searches and each lane searches only that window;
-//   * outputs (m, c) are written row-contiguous in i (coalesced), node 0 is the
-//     (1e-7, 1e-7) point (AS:1503-1504), and in solve mode the HARK distance
-//     (max |dm|, |dc|) is reduced per block and folded into a per-calibration slot
-//     with a 64-bit atomicMax on the bit pattern of the non-negative double.
+//     (once per current state s).  Here a 256-thread block owns one (calibration, M node
+//     k, tile of kTile = 64 asset nodes) and evaluates each
+//     V[s'][i] = R[k,s'] * c_{s'}(m'(i,k,s'), M'[k,s'])^-rho exactly once.
+//   * Phase 1: wave w handles next states s' = w, w + 4, ... for the 64 nodes of the
+//     tile, one node per lane.  Within a wave the queries m' = R a_i + W l(s') are
+//     increasing in the lane and all search the same two next-period rows (the M'
+//     bracket is wave-uniform), so the log-bucket index lookups and the bracket
+//     searches coalesce.  V goes to LDS [s'][i].
+//   * Phase 2: wave w handles current states s = w, w + 4, ...: E[s][i] =
+//     beta * sum_{s'} V[s'][i] P[s,s'] (AS:1485) in NumPy's pairwise order, V read from
+//     LDS (conflict-free), P[s,:] wave-uniform; then c = E^(-1/rho), m = a + c
+//     (AS:1490-1499), written row-contiguous in i (coalesced).  Node 0 is the
+//     (1e-7, 1e-7) point (AS:1503-1504).
+//   * In solve mode the HARK distance (max |dm|, |dc|) is reduced per block and folded
+//     into a per-calibration slot with a 64-bit atomicMax on the bit pattern of the
+//     non-negative double.
+// Splitting over (s', i) instead of one thread per node gives 4x the waves and a
+// 4x shorter dependent chain per lane (measured 1.0 ms -> see profiles/).
 #include "common.h"
 #include "internal.h"
 
@@ -29,7 +32,9 @@
 
 namespace aiy {
 
-constexpr int kEgmBlock = 128;
+constexpr int kEgmBlock = 256;
+constexpr int kTile = 64;                     // asset nodes per block (one per lane)
+constexpr int kEgmWaves = kEgmBlock / kWave;  // 4
 constexpr int kSlots = 4;  // per-calibration convergence words
 
 struct EgmDev {
@@ -45,30 +50,24 @@ struct EgmDev {
   const double* crra;
 };
 
-// Phase 1 + 2 of one EGM point (cal, k, i) for all S current states.  LOG selects
-// MargValueFuncCRRA/inversion with CRRA == 1 (NumPy's reciprocal fast path) at compile
-// time: with a runtime select the compiler evaluated the f64 pow unconditionally
-// (measured: 25k VALU instructions per wave, 1 ms per cycle at N_a = 10 000).
-template <int SMAX, bool TERMINAL, bool LOG>
-__device__ __forceinline__ double egm_point(const EgmDev& A, const double* __restrict__ m_next,
-                                            const double* __restrict__ c_next, double* __restrict__ m_out,
-                                            double* __restrict__ c_out, const int* __restrict__ idx_next, int cal,
-                                            int k, int i, bool active, bool track, double* Vs) {
+// Phase 1: V[s'][i] for s' = wave, wave + 4, ... (LOG: CRRA == 1 at compile time --
+// with a runtime select the compiler evaluated the f64 pow unconditionally, measured
+// 25k VALU instructions per wave).
+template <bool TERMINAL, bool LOG>
+__device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __restrict__ m_next,
+                                           const double* __restrict__ c_next, const int* __restrict__ idx_next,
+                                           int cal, int k, double a, bool active, double* Vs) {
   const int S = A.S, n_M = A.n_M, n_a = A.n_a, n1 = n_a + 1;
-  const double a = A.a_grid[(size_t)cal * n_a + (active ? i : n_a - 1)];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
   const double gam = A.crra[cal];
-  const double beta = A.beta[cal];
   const double* Rk = A.R_next + ((size_t)cal * n_M + k) * S;
   const double* Wk = A.W_next + ((size_t)cal * n_M + k) * S;
   const double* Mk = A.M_next + ((size_t)cal * n_M + k) * S;
   const double* lab = A.lab + (size_t)cal * S;
   const double* Mg = A.M_grid + (size_t)cal * n_M;
   const size_t tab_cal = (size_t)cal * S * n_M * n1;
-
-  // Phase 1 (runtime loop over s'): V[s'] = R * vP_{s'}(m', M') staged in LDS, one
-  // column per lane (conflict-free), so the unrolled contraction below can pull the
-  // whole vector into registers with compile-time indices.
-  for (int sp = 0; sp < S; ++sp) {
+  for (int sp = wave; sp < S; sp += kEgmWaves) {
     const double R = Rk[sp];
     const double q = R * a + Wk[sp] * lab[sp];  // mNextArray (AS:1024)
     double c;
@@ -95,18 +94,27 @@ __device__ __forceinline__ double egm_point(const EgmDev& A, const double* __res
       }
     }
     const double vP = LOG ? 1.0 / c : pow(c, -gam);  // MargValueFuncCRRA
-    Vs[sp * kEgmBlock + threadIdx.x] = R * vP;       // RnextArray * vPnext
+    Vs[sp * kTile + lane] = active ? R * vP : 0.0;   // RnextArray * vPnext
   }
-  double V[SMAX];
-#pragma unroll
-  for (int sp = 0; sp < SMAX; ++sp) V[sp] = (sp < S) ? Vs[sp * kEgmBlock + threadIdx.x] : 0.0;
+}
 
-  // Phase 2: E[s] = beta * sum_s' V[s'] P[s, s'] (NumPy pairwise order), invert, write.
-  const double* Pc = A.P + (size_t)cal * S * S;
+// Phase 2: outputs of current states s = wave, wave + 4, ...; returns the block-local
+// part of the HARK distance.
+template <int SMAX, bool LOG>
+__device__ __forceinline__ double egm_phase2(const EgmDev& A, const double* __restrict__ m_next,
+                                             const double* __restrict__ c_next, double* __restrict__ m_out,
+                                             double* __restrict__ c_out, int cal, int k, int i, double a,
+                                             bool active, bool track, const double* Vs, const double* Pl) {
+  const int S = A.S, n_M = A.n_M, n1 = A.n_a + 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const double gam = A.crra[cal];
+  const double beta = A.beta[cal];
+  const size_t tab_cal = (size_t)cal * S * n_M * n1;
   double dmax = 0.0;
-  for (int s = 0; s < S; ++s) {
-    const double* Ps = Pc + (size_t)s * S;
-    const double sum = np_pairwise_sum<SMAX>(S, [&](int t) { return V[t] * Ps[t]; });
+  for (int s = wave; s < S; s += kEgmWaves) {
+    const double* Ps = Pl + s * S;
+    const double sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vs[t * kTile + lane] * Ps[t]; });
     const double E = beta * sum;                              // EndOfPrdvP (AS:1485)
     const double c = LOG ? 1.0 / E : pow(E, -1.0 / gam);      // AS:1490
     const double m = a + c;                                   // AS:1499
@@ -149,25 +157,32 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
       return;
     }
   }
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ double Vs[SMAX * kTile];
+  __shared__ double Pl[SMAX * SMAX];
+  const int S = A.S;
+  const double* Pc = A.P + (size_t)cal * S * S;
+  for (int q = threadIdx.x; q < S * S; q += blockDim.x) Pl[q] = Pc[q];
+  const int i = blockIdx.x * kTile + (threadIdx.x & (kWave - 1));
   const bool active = i < A.n_a;
+  const double a = A.a_grid[(size_t)cal * A.n_a + (active ? i : A.n_a - 1)];
   const bool track = (dist_slots != nullptr) && cycle >= 2;
-  __shared__ double Vs[SMAX * kEgmBlock];
+  const bool log_util = A.crra[cal] == 1.0;   // block-uniform: one of two straight-line bodies
+  if (log_util) egm_phase1<TERMINAL, true>(A, m_next, c_next, idx_next, cal, k, a, active, Vs);
+  else egm_phase1<TERMINAL, false>(A, m_next, c_next, idx_next, cal, k, a, active, Vs);
+  __syncthreads();
   double dmax;
-  if (A.crra[cal] == 1.0)   // block-uniform: one of two straight-line bodies
-    dmax = egm_point<SMAX, TERMINAL, true>(A, m_next, c_next, m_out, c_out, idx_next, cal, k, i, active, track, Vs);
-  else
-    dmax = egm_point<SMAX, TERMINAL, false>(A, m_next, c_next, m_out, c_out, idx_next, cal, k, i, active, track, Vs);
+  if (log_util) dmax = egm_phase2<SMAX, true>(A, m_next, c_next, m_out, c_out, cal, k, i, a, active, track, Vs, Pl);
+  else dmax = egm_phase2<SMAX, false>(A, m_next, c_next, m_out, c_out, cal, k, i, a, active, track, Vs, Pl);
 
   if (dist_slots != nullptr) {
     if (track) {
-      __shared__ double red[kEgmBlock / kWave];
+      __shared__ double red[kEgmWaves];
       dmax = wave_nan_max(dmax);
       if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = dmax;
       __syncthreads();
       if (threadIdx.x == 0) {
         double d = red[0];
-        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) d = nan_max(d, red[w]);
+        for (int w = 1; w < kEgmWaves; ++w) d = nan_max(d, red[w]);
         atomicMax(&dist_slots[cal * kSlots + cycle % 3], (unsigned long long)__double_as_longlong(d));
       }
     }
@@ -226,7 +241,7 @@ static EgmDev to_dev(const aiy_egm_dims* d, const aiy_egm_inputs* in) {
 template <bool TERM>
 static void launch_cycle_t(const EgmDev& A, const double* mn, const double* cn, double* mo, double* co,
                            const int* ix, int cycle, unsigned long long* ds, int* lc, double tol, hipStream_t st) {
-  dim3 grid((A.n_a + kEgmBlock - 1) / kEgmBlock, A.n_M, A.n_cal);
+  dim3 grid((A.n_a + kTile - 1) / kTile, A.n_M, A.n_cal);
   dim3 block(kEgmBlock);
   if (A.S <= 8)
     hipLaunchKernelGGL((egm_cycle_kernel<8, TERM>), grid, block, 0, st, A, mn, cn, mo, co, ix, cycle, ds, lc, tol);

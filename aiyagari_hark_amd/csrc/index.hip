@@ -1,10 +1,11 @@
 // Build the log-bucket search index (common.h) of many policy rows at once.
 //
-// One lane per node i of a row (i = 0..n, n = n_a: the HARK search runs over x[:-1]):
-// with c(i) = clamp(key(x_i) - base, -1, K) and c(n) = K, lane i writes H[b] = i for
-// every bucket b in (c(i-1), c(i)].  The ranges partition [0, K], so every entry is
-// written exactly once and H[b] = first i with x_i >= edge_b -- a streaming pass, no
-// searches.  Starting the buckets at x[1] keeps the per-lane ranges short: the huge gap
+// One lane per node i of a row (i = 0..n-1, n = n_a: the HARK search runs over
+// x[:-1]): with c(i) = clamp(key(x_i) - base, -1, K - 1), lane i writes H[b] = i for
+// every bucket b in (c(i-1), c(i)]; lane n writes H[last + 1] = n and the header
+// last = c(n-1).  Every bucket up to last + 1 is written exactly once and
+// H[b] = first i with x_i >= edge_b -- a streaming pass, no searches.  Buckets above
+// last + 1 are never read (their queries exceed every node: lower_bound = n).  Starting the buckets at x[1] keeps the per-lane ranges short: the huge gap
 // between the 1e-7 borrowing node and the first real node is not bucketed.
 #include "common.h"
 #include "internal.h"
@@ -26,17 +27,23 @@ __global__ __launch_bounds__(256) void build_index_kernel(const double* __restri
     return;
   }
   const long long base = idx_key(x1);
-  // c(k): bucket of node k relative to base, -1 below bucket 0, capped at K; c(n) = K.
+  // c(k): bucket of node k relative to base, -1 below bucket 0, capped at K - 1.
   auto c = [&](int k) -> long long {
-    if (k >= n) return kIdxBuckets;
     const double v = xr[k];
     if (!(v > 0.0)) return -1;
     const long long b = idx_key(v) - base;
-    return b > kIdxBuckets ? kIdxBuckets : (b < -1 ? -1 : b);
+    return b > kIdxBuckets - 1 ? kIdxBuckets - 1 : (b < -1 ? -1 : b);
   };
-  const long long hi = c(i);
-  const long long lo = (i == 0) ? -1 : c(i - 1);
-  for (long long b = lo + 1; b <= hi; ++b) Hr[b] = i;
+  if (i < n) {
+    const long long hi = c(i);
+    const long long lo = (i == 0) ? -1 : c(i - 1);
+    for (long long b = lo + 1; b <= hi; ++b) Hr[b] = i;
+  } else {
+    // one bucket past the last node's (its lower_bound is n), and the header
+    const long long last = c(n - 1);
+    if (last + 1 <= kIdxBuckets - 1) Hr[last + 1] = n;
+    Hr[kIdxBuckets] = (int)last;
+  }
   if (i == 0) Hr[kIdxBuckets + 1] = (int)base;
 }
 

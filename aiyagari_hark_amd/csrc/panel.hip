@@ -100,8 +100,12 @@ __device__ __forceinline__ void index_window(const int* __restrict__ H, int base
   hi = n;
   if (H == nullptr || base == kIdxNoBase) return;
   const long long key = idx_key(q) - (long long)base;
+  const int last = H[kIdxBuckets];
   if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-  else if (key >= kIdxBuckets) { lo = H[kIdxBuckets]; hi = n; }
+  else if (key >= kIdxBuckets - 1) {
+    if (last == kIdxBuckets - 1) { lo = H[kIdxBuckets - 1]; hi = n; } else { lo = n; hi = n; }
+  }
+  else if (key > last) { lo = n; hi = n; }
   else { lo = H[key]; hi = H[key + 1]; }
   if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
 }

@@ -1,0 +1,69 @@
+"""Multi-GPU sharding, one process per GPU over torch.distributed.
+
+Two ways the path shards:
+
+* by calibration / shock stream (Table II sweep, bench.py): every rank solves its own
+  economies; no collective in the data path.  ``split_calibrations`` assigns them.
+* by agent population (configs[3], 1e8 agents): contiguous agent ranges per rank
+  (``shard_range``); every rank holds a replica of the policy table; the per-period
+  mean of end-of-period assets (``calc_R_and_W``, Aiyagari_Support.py:1868) becomes an
+  RCCL all-reduce of one double, enqueued by libaiyagari on the compute stream between
+  the per-period kernels (``bind_rccl`` + ``aiy_sim_periods``).  Philox shocks are
+  keyed by the GLOBAL agent index, so a sharded history equals the single-GPU one up
+  to the summation order of the mean.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def shard_range(n_total: int, world: int, rank: int):
+    """Contiguous, balanced agent range of ``rank``: (offset, n_local)."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    base, rem = divmod(int(n_total), int(world))
+    n_local = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, n_local
+
+
+def split_calibrations(items, world: int, rank: int):
+    """Round-robin assignment of independent calibrations to ranks."""
+    return [x for k, x in enumerate(items) if k % world == rank]
+
+
+def initial_labor_states(n_total: int, n_lab: int, offset: int, n_local: int):
+    """Even labour split of sim_birth (Aiyagari_Support.py:1203-1205) by global index
+    (state = global index // (n_total / n_lab)); the reference permutes it with the
+    agent RNG, which is immaterial for exchangeable agents and would need the whole
+    population on every rank."""
+    if n_total % n_lab:
+        raise ValueError("AgentCount must be a multiple of LaborStatesNo (AS:757)")
+    per = n_total // n_lab
+    return (np.arange(offset, offset + n_local) // per).astype(np.uint8)
+
+
+def bind_rccl(handle: "_lib.Handle", group=None):
+    """Create an RCCL communicator over the ranks of ``group`` and bind it to the
+    libaiyagari handle (rank 0 makes the ncclUniqueId, torch.distributed broadcasts it)."""
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        rc = handle.lib.aiy_comm_unique_id(buf)
+        if rc != _lib.AIY_OK:
+            raise _lib.AiyagariLibError("aiy_comm_unique_id failed")
+    obj = [bytes(buf.raw) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    uid = ctypes.create_string_buffer(obj[0], 128)
+    handle.check(handle.lib.aiy_comm_init(handle.h, uid, world, rank), "aiy_comm_init")
+    return world, rank
+
+
+def unbind_rccl(handle: "_lib.Handle"):
+    handle.check(handle.lib.aiy_comm_destroy(handle.h), "aiy_comm_destroy")
