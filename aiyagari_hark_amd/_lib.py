@@ -47,8 +47,8 @@ class Market(ctypes.Structure):
 
 class PanelModel(ctypes.Structure):
     _fields_ = [("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32), ("n_lab", ctypes.c_int32),
-                ("m_pol", vp), ("c_pol", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
-                ("mrkv_hist", vp), ("pol_index", vp)]
+                ("pol_pairs", vp), ("pol_index", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
+                ("mrkv_hist", vp)]
 
 
 # name -> (restype, argtypes)
@@ -72,6 +72,8 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_float), vp]),
     "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
     "aiy_index_ints_per_row": (ctypes.c_int32, []),
+    "aiy_panel_index_ints_per_row": (ctypes.c_int32, []),
+    "aiy_panel_prepare": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp, vp]),
     "aiy_build_index": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]),
     "aiy_comm_unique_id": (ctypes.c_int32, [vp]),
     "aiy_comm_init": (ctypes.c_int32, [vp, vp, ctypes.c_int32, ctypes.c_int32]),

@@ -114,41 +114,58 @@ __device__ __forceinline__ double interp_row(const double* __restrict__ x, const
 // ---------------------------------------------------------------------------------
 // Log-bucket search index of a sorted, positive row x[0..n) (the m nodes of one
 // LinearInterp, searched over x[:-1]).  Bucket b covers the doubles whose bit
-// pattern >> kIdxShift equals base + b, base = key(x[1]) (x[0] is the 1e-7 borrowing
-// node, far below the rest of the row): kIdxPerOctave buckets per binary octave.
+// pattern >> SHIFT equals base + b, base = key(x[1]) (x[0] is the 1e-7 borrowing node,
+// far below the rest of the row): 2^(52 - SHIFT) buckets per binary octave.
 // H[b] = first i with x[i] >= edge_b = lower_bound(x, edge_b).  A query in bucket b has
 // its lower_bound in [H[b], H[b+1]] (queries below edge_0: [0, H[0]]; above the last
 // node's bucket: n), found exactly -- bucket edges are bit-level, no floating-point
 // rounding -- by a search over a handful of nodes.
-//   layout per row: H[0 .. kIdxBuckets - 1] buckets (entries up to last + 1 valid),
-//   last = bucket of the last node at [kIdxBuckets], base at [kIdxBuckets + 1]
+//   layout per row: H[0 .. BUCKETS - 1] (entries up to last + 1 valid),
+//   last = bucket of the last node at [BUCKETS], base at [BUCKETS + 1]
+// EgmIdx (256 / octave) is rebuilt every EGM cycle; PanelIdx (2048 / octave) is built
+// once per history and leaves ~1 node per bucket, so a panel lookup is one index line
+// plus one (x, c) pair line.
 // ---------------------------------------------------------------------------------
-constexpr int kIdxShift = 44;                   // 8 mantissa bits -> 256 buckets / octave
-constexpr int kIdxBuckets = 16 * 256;           // 16 octaves above x[1]
-constexpr int kIdxRow = kIdxBuckets + 2;        // ints per row
+template <int SHIFT, int BUCKETS>
+struct IdxSpec {
+  static constexpr int kShift = SHIFT;
+  static constexpr int kBuckets = BUCKETS;
+  static constexpr int kRow = BUCKETS + 2;   // ints per row
+};
+using EgmIdx = IdxSpec<44, 16 * 256>;
+using PanelIdx = IdxSpec<41, 16 * 2048>;
+constexpr int kIdxShift = EgmIdx::kShift;
+constexpr int kIdxBuckets = EgmIdx::kBuckets;
+constexpr int kIdxRow = EgmIdx::kRow;
 constexpr int kIdxNoBase = -2147483647 - 1;     // x[1] <= 0 or n < 2: index unusable -> full search
 
+template <class I = EgmIdx>
 __device__ __forceinline__ long long idx_key(double q) {
-  return (long long)(__double_as_longlong(q) >> kIdxShift);
+  return (long long)(__double_as_longlong(q) >> I::kShift);
+}
+
+// Search window [lo, hi) of lower_bound(x[0..n), q) from the row index H (base given).
+template <class I>
+__device__ __forceinline__ void index_window(const int* __restrict__ H, int base, int n, double q, int& lo, int& hi) {
+  lo = 0;
+  hi = n;
+  if (H == nullptr || base == kIdxNoBase) return;
+  const long long key = idx_key<I>(q) - (long long)base;
+  const int last = H[I::kBuckets];
+  if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
+  else if (key >= I::kBuckets - 1) {                    // capped top bucket / beyond the span
+    if (last == I::kBuckets - 1) { lo = H[I::kBuckets - 1]; hi = n; } else { lo = n; hi = n; }
+  }
+  else if (key > last) { lo = n; hi = n; }              // above every node
+  else { lo = H[key]; hi = H[key + 1]; }
+  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }  // defensive: unsorted rows
 }
 
 // lower_bound(x[0..n), q) using the row index H (nullptr -> plain binary search).
+template <class I = EgmIdx>
 __device__ __forceinline__ int locate(const double* __restrict__ x, int n, const int* __restrict__ H, double q) {
   int lo = 0, hi = n;
-  if (H != nullptr) {
-    const int base = H[kIdxBuckets + 1];
-    if (base != kIdxNoBase) {
-      const long long key = idx_key(q) - (long long)base;
-      const int last = H[kIdxBuckets];
-      if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-      else if (key >= kIdxBuckets - 1) {                    // capped top bucket / beyond the span
-        if (last == kIdxBuckets - 1) { lo = H[kIdxBuckets - 1]; hi = n; } else { lo = n; hi = n; }
-      }
-      else if (key > last) { lo = n; hi = n; }              // above every node
-      else { lo = H[key]; hi = H[key + 1]; }
-      if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }   // defensive: unsorted rows
-    }
-  }
+  if (H != nullptr) index_window<I>(H, H[I::kBuckets + 1], n, q, lo, hi);
   return lower_bound(x, lo, hi, q);
 }
 

@@ -12,27 +12,29 @@
 
 namespace aiy {
 
-__global__ __launch_bounds__(256) void build_index_kernel(const double* __restrict__ x, long long n_rows, int n1,
-                                                          int* __restrict__ H) {
+template <class I>
+__global__ __launch_bounds__(256) void build_index_kernel(const double* __restrict__ x, long long stride, long long n_rows,
+                                                          int n1, int* __restrict__ H) {
   const long long row = blockIdx.y + (long long)blockIdx.z * gridDim.y;
   if (row >= n_rows) return;
   const int n = n1 - 1;
-  const double* xr = x + row * n1;
-  int* Hr = H + row * kIdxRow;
+  const double* xr0 = x + row * n1 * stride;
+  auto xr = [&](int k) { return xr0[(size_t)k * stride]; };
+  int* Hr = H + row * I::kRow;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n) return;
-  const double x1 = n >= 2 ? xr[1] : 0.0;
+  const double x1 = n >= 2 ? xr(1) : 0.0;
   if (!(x1 > 0.0)) {
-    if (i == 0) Hr[kIdxBuckets + 1] = kIdxNoBase;
+    if (i == 0) Hr[I::kBuckets + 1] = kIdxNoBase;
     return;
   }
-  const long long base = idx_key(x1);
+  const long long base = idx_key<I>(x1);
   // c(k): bucket of node k relative to base, -1 below bucket 0, capped at K - 1.
   auto c = [&](int k) -> long long {
-    const double v = xr[k];
+    const double v = xr(k);
     if (!(v > 0.0)) return -1;
-    const long long b = idx_key(v) - base;
-    return b > kIdxBuckets - 1 ? kIdxBuckets - 1 : (b < -1 ? -1 : b);
+    const long long b = idx_key<I>(v) - base;
+    return b > I::kBuckets - 1 ? I::kBuckets - 1 : (b < -1 ? -1 : b);
   };
   if (i < n) {
     const long long hi = c(i);
@@ -41,10 +43,10 @@ __global__ __launch_bounds__(256) void build_index_kernel(const double* __restri
   } else {
     // one bucket past the last node's (its lower_bound is n), and the header
     const long long last = c(n - 1);
-    if (last + 1 <= kIdxBuckets - 1) Hr[last + 1] = n;
-    Hr[kIdxBuckets] = (int)last;
+    if (last + 1 <= I::kBuckets - 1) Hr[last + 1] = n;
+    Hr[I::kBuckets] = (int)last;
   }
-  if (i == 0) Hr[kIdxBuckets + 1] = (int)base;
+  if (i == 0) Hr[I::kBuckets + 1] = (int)base;
 }
 
 int32_t launch_build_index(aiy_handle* h, const double* x, long long n_rows, int n1, int* H, hipStream_t st) {
@@ -52,12 +54,39 @@ int32_t launch_build_index(aiy_handle* h, const double* x, long long n_rows, int
   const long long gy = n_rows < 65535 ? n_rows : 65535;
   const long long gz = (n_rows + gy - 1) / gy;
   dim3 grid((n1 + 255) / 256, (unsigned)gy, (unsigned)gz);
-  hipLaunchKernelGGL(build_index_kernel, grid, dim3(256), 0, st, x, n_rows, n1, H);
+  hipLaunchKernelGGL(build_index_kernel<EgmIdx>, grid, dim3(256), 0, st, x, 1LL, n_rows, n1, H);
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
 }
 
+// Interleave a policy table into (m, c) pairs and build its fine panel index.
+__global__ __launch_bounds__(256) void interleave_kernel(const double* __restrict__ m, const double* __restrict__ c,
+                                                         long long n, double* __restrict__ pairs) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  reinterpret_cast<double2*>(pairs)[t] = make_double2(m[t], c[t]);
+}
+
 }  // namespace aiy
+
+extern "C" int32_t aiy_panel_index_ints_per_row(void) { return aiy::PanelIdx::kRow; }
+
+extern "C" int32_t aiy_panel_prepare(aiy_handle* h, int64_t n_rows, int32_t n1, const double* m_pol,
+                                     const double* c_pol, double* pairs, int32_t* index, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (n_rows < 1 || n1 < 2 || !m_pol || !c_pol || !pairs || !index) return aiy::fail(h, AIY_ERR_ARG, "bad prepare args");
+  AIY_HIP(h, hipSetDevice(h->device));
+  hipStream_t st = aiy::as_stream(stream);
+  const long long n = n_rows * (long long)n1;
+  hipLaunchKernelGGL(aiy::interleave_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, m_pol, c_pol, n, pairs);
+  const long long gy = n_rows < 65535 ? n_rows : 65535;
+  const long long gz = (n_rows + gy - 1) / gy;
+  dim3 grid((n1 + 255) / 256, (unsigned)gy, (unsigned)gz);
+  hipLaunchKernelGGL(aiy::build_index_kernel<aiy::PanelIdx>, grid, dim3(256), 0, st, pairs, 2LL, (long long)n_rows, n1,
+                     index);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
 
 extern "C" int32_t aiy_index_ints_per_row(void) { return aiy::kIdxRow; }
 

@@ -29,13 +29,12 @@ constexpr int kGraphPeriods = 64;
 
 struct PanelDev {
   int S, n_M, n_a, n_lab;
-  const double* m_pol;
-  const double* c_pol;
   const double* M_grid;
   const double* lab_level;
   const double* lab_cdf;
   const int* mrkv_hist;
-  const int* pol_index;
+  const int* pol_index;     // PanelIdx rows (aiy_panel_prepare)
+  const double2* pol_pairs; // (m, c) interleaved rows (aiy_panel_prepare)
 };
 
 struct PanelRun {
@@ -80,37 +79,32 @@ __device__ __forceinline__ void mill(const aiy_market& mk, const int* mrkv_hist,
   if (hist_M) hist_M[t] = Mnow;
 }
 
-// Two LinearInterp bracket searches (rows j-1 and j of one state) advanced in
-// lock-step so their dependent loads overlap; each starts from its index window.
-__device__ __forceinline__ void locate2(const double* __restrict__ x0, const double* __restrict__ x1, int& lo0,
+// Two LinearInterp bracket searches over interleaved (m, c) rows (rows j-1 and j of
+// one state) advanced in lock-step so their dependent loads overlap.
+__device__ __forceinline__ void locate2(const double2* __restrict__ p0, const double2* __restrict__ p1, int& lo0,
                                         int hi0, int& lo1, int hi1, double q) {
   while (lo0 < hi0 || lo1 < hi1) {
     const int m0 = lo0 + ((hi0 - lo0) >> 1);
     const int m1 = lo1 + ((hi1 - lo1) >> 1);
     const bool a0 = lo0 < hi0, a1 = lo1 < hi1;
-    const double v0 = a0 ? x0[m0] : 0.0;
-    const double v1 = a1 ? x1[m1] : 0.0;
+    const double v0 = a0 ? p0[m0].x : 0.0;
+    const double v1 = a1 ? p1[m1].x : 0.0;
     if (a0) { if (v0 < q) lo0 = m0 + 1; else hi0 = m0; }
     if (a1) { if (v1 < q) lo1 = m1 + 1; else hi1 = m1; }
   }
 }
 
-__device__ __forceinline__ void index_window(const int* __restrict__ H, int base, int n, double q, int& lo, int& hi) {
-  lo = 0;
-  hi = n;
-  if (H == nullptr || base == kIdxNoBase) return;
-  const long long key = idx_key(q) - (long long)base;
-  const int last = H[kIdxBuckets];
-  if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-  else if (key >= kIdxBuckets - 1) {
-    if (last == kIdxBuckets - 1) { lo = H[kIdxBuckets - 1]; hi = n; } else { lo = n; hi = n; }
-  }
-  else if (key > last) { lo = n; hi = n; }
-  else { lo = H[key]; hi = H[key + 1]; }
-  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
+// HARK LinearInterp at bracket i of an interleaved row (x0 = first node).
+__device__ __forceinline__ double lerp_pair(const double2* __restrict__ p, int i, double q, double x0) {
+  const double2 lo = p[i - 1], hi = p[i];
+  const double alpha = (q - lo.x) / (hi.x - lo.x);
+  const double v = (1.0 - alpha) * lo.y + alpha * hi.y;
+  return (q < x0) ? __builtin_nan("") : v;
 }
 
-constexpr int kLdsLab = 16;   // labour chains up to 16 states are staged in LDS
+constexpr int kLdsLab = 16;
+
+__device__ __forceinline__ double kBorrowNodeOf(const double2* p) { return p[0].x; }   // labour chains up to 16 states are staged in LDS
 
 __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, PanelRun r, aiy_market mk) {
   const double Mnow = load_f64_agent(&r.sow[0]);
@@ -143,8 +137,8 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
     for (int q = threadIdx.x; q < n_lab; q += blockDim.x) {
       s_lvl[q] = P.lab_level[q];
       const int s = 4 * q + 2 * Mrkv + 1;
-      s_base[2 * q] = P.pol_index ? P.pol_index[((size_t)s * n_M + jlo) * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
-      s_base[2 * q + 1] = P.pol_index ? P.pol_index[((size_t)s * n_M + jhi) * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
+      s_base[2 * q] = P.pol_index[((size_t)s * n_M + jlo) * PanelIdx::kRow + PanelIdx::kBuckets + 1];
+      s_base[2 * q + 1] = P.pol_index[((size_t)s * n_M + jhi) * PanelIdx::kRow + PanelIdx::kBuckets + 1];
     }
   }
   __syncthreads();
@@ -165,24 +159,23 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
     const double m = Rnow * a_prev + Wnow * (lvl * 1.0);                 // AS:1283
     const int s = 4 * ln + 2 * Mrkv + 1;                                 // employed (Urate = 0)
     const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
-    const double* x0 = P.m_pol + r0 * n1;
-    const double* x1 = P.m_pol + r1 * n1;
+    const double2* p0 = P.pol_pairs + r0 * n1;
+    const double2* p1 = P.pol_pairs + r1 * n1;
+    const int* H0 = P.pol_index + r0 * PanelIdx::kRow;
+    const int* H1 = P.pol_index + r1 * PanelIdx::kRow;
     int b0, b1;
     if (lds_lab) { b0 = s_base[2 * ln]; b1 = s_base[2 * ln + 1]; }
-    else {
-      b0 = P.pol_index ? P.pol_index[r0 * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
-      b1 = P.pol_index ? P.pol_index[r1 * kIdxRow + kIdxBuckets + 1] : kIdxNoBase;
-    }
+    else { b0 = H0[PanelIdx::kBuckets + 1]; b1 = H1[PanelIdx::kBuckets + 1]; }
     int lo0, hi0, lo1, hi1;
-    index_window(P.pol_index ? P.pol_index + r0 * kIdxRow : nullptr, b0, n_a, m, lo0, hi0);
-    index_window(P.pol_index ? P.pol_index + r1 * kIdxRow : nullptr, b1, n_a, m, lo1, hi1);
-    locate2(x0, x1, lo0, hi0, lo1, hi1, m);
+    index_window<PanelIdx>(H0, b0, n_a, m, lo0, hi0);
+    index_window<PanelIdx>(H1, b1, n_a, m, lo1, hi1);
+    locate2(p0, p1, lo0, hi0, lo1, hi1, m);
     const int i0 = lo0 < 1 ? 1 : lo0;
     const int i1 = lo1 < 1 ? 1 : lo1;
-    const double f0 = lerp_at(x0, P.c_pol + r0 * n1, i0, m, x0[0]);
+    const double f0 = lerp_pair(p0, i0, m, kBorrowNodeOf(p0));
     double c = f0;
     if (n_M > 1) {
-      const double f1 = lerp_at(x1, P.c_pol + r1 * n1, i1, m, x1[0]);
+      const double f1 = lerp_pair(p1, i1, m, kBorrowNodeOf(p1));
       c = (1 - alpha) * f0 + alpha * f1;                                 // LinearInterpOnInterp1D
     }
     const double an = m - c;                                             // AS:1415
@@ -287,8 +280,8 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   if (model->S < 1 || model->n_M < 1 || model->n_a < 2 || model->n_lab < 1 || model->n_lab > 255)
     return fail(h, AIY_ERR_ARG, "bad model sizes");
   if (model->S < 4 * model->n_lab) return fail(h, AIY_ERR_ARG, "S must be 4 * n_lab (KS form)");
-  if (!model->m_pol || !model->c_pol || !model->lab_level || !model->lab_cdf || !model->mrkv_hist)
-    return fail(h, AIY_ERR_ARG, "null model array");
+  if (!model->lab_level || !model->lab_cdf || !model->mrkv_hist || !model->pol_pairs || !model->pol_index)
+    return fail(h, AIY_ERR_ARG, "null model array (pol_pairs/pol_index come from aiy_panel_prepare)");
   if (model->n_M > 1 && !model->M_grid) return fail(h, AIY_ERR_ARG, "null M_grid");
   if (n_local < 0 || n_total < 1 || agent_offset < 0) return fail(h, AIY_ERR_ARG, "bad agent counts");
   if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
@@ -304,9 +297,9 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   const int nb = sim_blocks(n_local);
   PanelDev P;
   P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
-  P.m_pol = model->m_pol; P.c_pol = model->c_pol; P.M_grid = model->M_grid;
+  P.M_grid = model->M_grid;
   P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
-  P.pol_index = model->pol_index;
+  P.pol_index = model->pol_index; P.pol_pairs = reinterpret_cast<const double2*>(model->pol_pairs);
   PanelRun r;
   r.n = n_local; r.offset = agent_offset; r.n_total = n_total; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld;
   r.u_t0 = t0; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
@@ -362,9 +355,9 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   hipStream_t st = as_stream(stream);
   PanelDev P;
   P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
-  P.m_pol = model->m_pol; P.c_pol = model->c_pol; P.M_grid = model->M_grid;
+  P.M_grid = model->M_grid;
   P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
-  P.pol_index = model->pol_index;
+  P.pol_index = model->pol_index; P.pol_pairs = reinterpret_cast<const double2*>(model->pol_pairs);
   PanelRun r;
   r.n = n_local; r.offset = 0; r.n_total = n_local; r.a = a; r.lab = lab; r.u = nullptr; r.u_ld = 0; r.u_t0 = 0;
   r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;

@@ -56,15 +56,17 @@ class DevicePanel:
         keep = dict(m_pol=m_pol.contiguous(), c_pol=c_pol.contiguous(), M_grid=M_grid.contiguous(),
                     lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
                     mrkv_hist=mrkv_hist.to(torch.int32).contiguous())
-        # log-bucket search index of every policy row (built on device, once per history)
+        # interleaved (m, c) pairs + fine log-bucket search index (built on device once per history)
         h = _lib.handle(self.device.index)
-        ipr = h.lib.aiy_index_ints_per_row()
+        ipr = h.lib.aiy_panel_index_ints_per_row()
+        keep["pol_pairs"] = torch.empty((S, n_M, n1, 2), dtype=F64, device=self.device)
         keep["pol_index"] = torch.empty((S * n_M, ipr), dtype=torch.int32, device=self.device)
-        h.check(h.lib.aiy_build_index(h.h, S * n_M, n1, _lib.ptr(keep["m_pol"]), _lib.ptr(keep["pol_index"]),
-                                      _lib.stream_ptr()), "aiy_build_index")
+        h.check(h.lib.aiy_panel_prepare(h.h, S * n_M, n1, _lib.ptr(keep["m_pol"]), _lib.ptr(keep["c_pol"]),
+                                        _lib.ptr(keep["pol_pairs"]), _lib.ptr(keep["pol_index"]), _lib.stream_ptr()),
+                "aiy_panel_prepare")
         pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
-                                                       ("m_pol", "c_pol", "M_grid", "lab_level", "lab_cdf",
-                                                        "mrkv_hist", "pol_index")))
+                                                       ("pol_pairs", "pol_index", "M_grid", "lab_level", "lab_cdf",
+                                                        "mrkv_hist")))
         mk = _lib.Market(market["CapShare"], market["DeprFac"], (ctypes.c_double * 2)(*market["prod"]),
                          (ctypes.c_double * 2)(*market["agg_L"]))
         self._model = (pm, mk, keep)

@@ -133,15 +133,22 @@ typedef struct {
 /* Household panel model for one calibration (policy fixed during a history). */
 typedef struct {
   int32_t S, n_M, n_a, n_lab;
-  const double* m_pol;     /* [S][n_M][n_a+1] converged policy (AiyagariType.solution[0]) */
-  const double* c_pol;     /* [S][n_M][n_a+1]                                             */
-  const double* M_grid;    /* [n_M]                                                       */
-  const double* lab_level; /* [n_lab] LSStates (AS:1265)                                  */
-  const double* lab_cdf;   /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
-  const int32_t* mrkv_hist;/* [act_T] MrkvNow_hist (AS:1793-1805)                          */
-  const int32_t* pol_index;/* [S][n_M][aiy_index_ints_per_row()] from aiy_build_index(m_pol),
-                              or NULL (plain binary search)                                 */
+  const double* pol_pairs;  /* [S][n_M][n_a+1][2] (m, c) pairs of the converged policy
+                               (AiyagariType.solution[0]), from aiy_panel_prepare          */
+  const int32_t* pol_index; /* [S][n_M][aiy_panel_index_ints_per_row()], aiy_panel_prepare */
+  const double* M_grid;     /* [n_M]                                                       */
+  const double* lab_level;  /* [n_lab] LSStates (AS:1265)                                  */
+  const double* lab_cdf;    /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
+  const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805)                          */
 } aiy_panel_model;
+
+/* Prepare a policy table [n_rows = S * n_M][n1] for the panel: interleave (m, c) into
+ * pairs [n_rows][n1][2] and build a fine log-bucket search index of every row (about one
+ * node per bucket, so a panel lookup touches one index line and one pair line).
+ * Asynchronous. */
+int32_t aiy_panel_index_ints_per_row(void);
+int32_t aiy_panel_prepare(aiy_handle* h, int64_t n_rows, int32_t n1, const double* m_pol,
+                          const double* c_pol, double* pairs, int32_t* index, aiy_stream stream);
 
 /* Device-resident market state ("sow_state", AS:1585), 8 doubles:
  *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] sum(a) [7] period index t */
