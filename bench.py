@@ -64,9 +64,9 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def make_economy(seed, n_agents, n_a, act_T, device):
+def make_economy(seed, n_agents, n_a, act_T, device, t_discard=T_DISCARD):
     from aiyagari_hark_amd.model import AiyagariEconomy, AiyagariType
-    econ_d = dict(act_T=act_T, T_discard=T_DISCARD, LaborAR=0.6, LaborSD=0.2, CRRA=1.0,
+    econ_d = dict(act_T=act_T, T_discard=t_discard, LaborAR=0.6, LaborSD=0.2, CRRA=1.0,
                   intercept_prev=[0.0, 0.0], slope_prev=[1.0, 1.0])
     agent_d = dict(LaborAR=0.6, LaborSD=0.2, CRRA=1.0, aCount=n_a, AgentCount=n_agents)
     econ = AiyagariEconomy(**econ_d)
@@ -158,6 +158,18 @@ def egm_kernel_time(agent, n_launch=20):
     return ms.value / n_launch
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return float(d[kernel]["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
 def cpu_baseline(n_ge, cycles_per_solve, budget_s=20.0):
     """The oracle (NumPy restatement of the reference path at HARK's vectorisation
     granularity) timed on this host on a bounded sample of the same workload: EGM cycles
@@ -202,6 +214,7 @@ def main():
     ap.add_argument("--agents", type=int, default=N_AGENTS)
     ap.add_argument("--grid", type=int, default=N_A)
     ap.add_argument("--act-T", type=int, default=ACT_T)
+    ap.add_argument("--t-discard", type=int, default=T_DISCARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -212,7 +225,8 @@ def main():
         build.build(verbose=False)
     barrier(world)
 
-    econ, agent = make_economy(seed=rank, n_agents=args.agents, n_a=args.grid, act_T=args.act_T, device=dev)
+    econ, agent = make_economy(seed=rank, n_agents=args.agents, n_a=args.grid, act_T=args.act_T, device=dev,
+                               t_discard=args.t_discard)
     for _ in range(args.warmup):
         run_step(econ, agent, Probe())
     probe = Probe()
@@ -273,7 +287,7 @@ def main():
                      "bound": "hbm", "achieved": panel_gbs if panel_share >= 0.5 else egm_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (panel_gbs if panel_share >= 0.5 else egm_gbs) / HBM_PEAK_GBS,
-                     "traffic": None,
+                     "traffic": pmc_traffic("sim_period_kernel" if panel_share >= 0.5 else "egm_cycle_kernel"),
                      "algorithmic_bytes_per_launch": panel_bytes if panel_share >= 0.5 else egm_bytes,
                      "avg_launch_ms": t_panel_ms if panel_share >= 0.5 else t_egm_ms},
         "roofline_other": {"kernel": "egm_cycle_kernel" if panel_share >= 0.5 else "sim_period_kernel",

@@ -1,0 +1,51 @@
+"""Summarise rocprofv3 PMC passes into per-launch HBM traffic for bench.py.
+
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json>
+
+FETCH_SIZE and WRITE_SIZE (KB) come from separate rocprofv3 --pmc passes (they do not
+fit one pass on gfx950).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the
+bytes of a wide coalesced streaming read on gfx950, so it is doubled; WRITE_SIZE is
+exact for streaming stores.  Both are averaged per dispatch of each kernel.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"]
+            tot[k] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: (tot[k] / len(disp[k]), len(disp[k])) for k in tot}
+
+
+def main():
+    fd, wd, out = sys.argv[1:4]
+    fetch = per_kernel(fd, "FETCH_SIZE")
+    write = per_kernel(wd, "WRITE_SIZE")
+    res = {}
+    for k in set(fetch) | set(write):
+        f_kb, nf = fetch.get(k, (0.0, 0))
+        w_kb, nw = write.get(k, (0.0, 0))
+        short = k.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+        res[short] = dict(kernel=k, fetch_kb_raw=f_kb, write_kb=w_kb, dispatches=[nf, nw],
+                          hbm_bytes_per_launch=(2.0 * f_kb + w_kb) * 1024.0,
+                          correction="FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1")
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print(f"{k}: {v['hbm_bytes_per_launch'] / 1e6:.2f} MB/launch (fetch raw {v['fetch_kb_raw']:.0f} KB, "
+              f"write {v['write_kb']:.0f} KB)")
+
+
+if __name__ == "__main__":
+    main()
