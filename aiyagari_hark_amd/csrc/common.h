@@ -242,11 +242,19 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
 }
-__device__ __forceinline__ double philox_uniform(uint32_t ctr0, uint64_t idx, uint64_t seed, uint32_t stream) {
-  uint32_t c[4] = {ctr0, (uint32_t)idx, (uint32_t)(idx >> 32), stream};
+// One Philox call per agent PAIR (2j, 2j + 1): counter = (ctr0, j, 0, stream); words
+// (0, 1) give agent 2j's 53-bit uniform, words (2, 3) agent 2j+1's.
+__device__ __forceinline__ void philox_uniform2(uint32_t ctr0, uint64_t pair, uint64_t seed, uint32_t stream,
+                                                double& u_even, double& u_odd) {
+  uint32_t c[4] = {ctr0, (uint32_t)pair, (uint32_t)(pair >> 32), stream};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  double a = (double)(c[0] >> 5), b = (double)(c[1] >> 6);
-  return (a * 67108864.0 + b) / 9007199254740992.0;
+  u_even = ((double)(c[0] >> 5) * 67108864.0 + (double)(c[1] >> 6)) / 9007199254740992.0;
+  u_odd = ((double)(c[2] >> 5) * 67108864.0 + (double)(c[3] >> 6)) / 9007199254740992.0;
+}
+__device__ __forceinline__ double philox_uniform(uint32_t ctr0, uint64_t idx, uint64_t seed, uint32_t stream) {
+  double e, o;
+  philox_uniform2(ctr0, idx >> 1, seed, stream, e, o);
+  return (idx & 1) ? o : e;
 }
 
 }  // namespace aiy

@@ -35,7 +35,12 @@ namespace aiy {
 constexpr int kEgmBlock = 256;
 constexpr int kTile = 64;                     // asset nodes per block (one per lane)
 constexpr int kEgmWaves = kEgmBlock / kWave;  // 4
-constexpr int kSlots = 4;  // per-calibration convergence words
+// Per-calibration convergence words: 3 rotating distance slots x kSub sub-slots (block b
+// folds into sub-slot b % kSub, so ~2 400 blocks do not serialise on one address), then
+// the sticky converged flag.
+constexpr int kSub = 32;
+constexpr int kFlag = 3 * kSub;
+constexpr int kSlots = 3 * kSub + 4;
 
 struct EgmDev {
   int n_cal, S, n_M, n_a;
@@ -150,12 +155,21 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
   const int k = blockIdx.y;
   if (dist_slots != nullptr && cycle >= 3) {
     unsigned long long* slots = dist_slots + cal * kSlots;
-    if (load_u64_agent(&slots[3]) != 0ull) return;   // converged earlier (sticky flag)
-    const double dprev = __longlong_as_double((long long)load_u64_agent(&slots[(cycle - 1) % 3]));
-    if (!(dprev > tol)) {
-      if (blockIdx.x == 0 && k == 0 && threadIdx.x == 0) store_u64_agent(&slots[3], 1ull);
-      return;
+    __shared__ int s_skip;
+    if (threadIdx.x < kWave) {
+      const bool done = load_u64_agent(&slots[kFlag]) != 0ull;   // converged earlier (sticky flag)
+      double d = 0.0;
+      if (threadIdx.x < kSub)
+        d = __longlong_as_double((long long)load_u64_agent(&slots[((cycle - 1) % 3) * kSub + threadIdx.x]));
+      d = wave_nan_max(d);
+      if (threadIdx.x == 0) {
+        const bool skip = done || !(d > tol);
+        s_skip = skip ? 1 : 0;
+        if (skip && !done && blockIdx.x == 0 && k == 0) store_u64_agent(&slots[kFlag], 1ull);
+      }
     }
+    __syncthreads();
+    if (s_skip) return;
   }
   __shared__ double Vs[SMAX * kTile];
   __shared__ double Pl[SMAX * SMAX];
@@ -183,12 +197,14 @@ __global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const do
       if (threadIdx.x == 0) {
         double d = red[0];
         for (int w = 1; w < kEgmWaves; ++w) d = nan_max(d, red[w]);
-        atomicMax(&dist_slots[cal * kSlots + cycle % 3], (unsigned long long)__double_as_longlong(d));
+        const int b = blockIdx.x + gridDim.x * blockIdx.y;
+        atomicMax(&dist_slots[cal * kSlots + (cycle % 3) * kSub + (b % kSub)],
+                  (unsigned long long)__double_as_longlong(d));
       }
     }
-    if (blockIdx.x == 0 && k == 0 && threadIdx.x == 0) {
-      store_u64_agent(&dist_slots[cal * kSlots + (cycle + 1) % 3], 0ull);
-      last_cycle[cal] = cycle;
+    if (blockIdx.x == 0 && k == 0) {
+      if (threadIdx.x < kSub) store_u64_agent(&dist_slots[cal * kSlots + ((cycle + 1) % 3) * kSub + threadIdx.x], 0ull);
+      if (threadIdx.x == 0) last_cycle[cal] = cycle;
     }
   }
 }
@@ -215,6 +231,18 @@ __global__ void policy_eval_kernel(int S, int n_M, int n_a, const double* __rest
   const double f0 = interp_row(bm + (size_t)(j - 1) * n1, bc + (size_t)(j - 1) * n1, n_a, q);
   const double f1 = interp_row(bm + (size_t)j * n1, bc + (size_t)j * n1, n_a, q);
   out[t] = (1 - alpha) * f0 + alpha * f1;
+}
+
+// Host: the distance of cycle `last` = max over its sub-slots (NaN-propagating).
+static double slot_max(const unsigned long long* slots, int last) {
+  double d = 0.0;
+  for (int q = 0; q < kSub; ++q) {
+    double v;
+    unsigned long long b = slots[(last % 3) * kSub + q];
+    std::memcpy(&v, &b, sizeof(v));
+    d = (v != v || v > d) ? v : d;
+  }
+  return d;
 }
 
 static int32_t check_egm(aiy_handle* h, const aiy_egm_dims* d, const aiy_egm_inputs* in) {
@@ -352,9 +380,7 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
     bool all = true;
     for (int c = 0; c < n_cal; ++c) {
       const int last = h->h_last[c];
-      double d;
-      unsigned long long bits = h->h_dist[c * kSlots + last % 3];
-      memcpy(&d, &bits, sizeof(d));
+      const double d = slot_max(h->h_dist + (size_t)c * kSlots, last);
       const bool conv = (last >= 2 && !(d > tol)) || last >= last_allowed;
       all = all && conv;
     }
@@ -363,9 +389,7 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   }
   for (int c = 0; c < n_cal; ++c) {
     const int last = h->h_last[c];
-    unsigned long long bits = h->h_dist[c * kSlots + last % 3];
-    double d;
-    memcpy(&d, &bits, sizeof(d));
+    const double d = slot_max(h->h_dist + (size_t)c * kSlots, last);
     cycles_out[c] = last;
     dist_out[c] = last >= 2 ? d : 100.0;
     const size_t off = (size_t)c * per_cal;

@@ -6,9 +6,12 @@ in period t from a counter-based Philox4x32-10 generator (Salmon et al., SC'11,
 SURVEY.md §8d config 2.  This module restates it bit-exactly so tests can pin the
 device stream:
 
-    counter = (t, i_lo, i_hi, stream), key = (seed_lo, seed_hi)
+    counter = (t, j_lo, j_hi, stream), j = i // 2, key = (seed_lo, seed_hi)
     (x0, x1, x2, x3) = philox4x32_10(counter, key)
-    u = ((x0 >> 5) * 2**26 + (x1 >> 6)) / 2**53          # in [0, 1), 53 random bits
+    u(2j)     = ((x0 >> 5) * 2**26 + (x1 >> 6)) / 2**53   # in [0, 1), 53 random bits
+    u(2j + 1) = ((x2 >> 5) * 2**26 + (x3 >> 6)) / 2**53
+
+(one Philox call serves two agents; every agent still gets its own 53-bit uniform)
 
 (the same 53-bit construction NumPy's MT19937 ``random_sample`` uses).
 """
@@ -47,14 +50,16 @@ def uniform(t, idx, seed, stream=0):
     idx = np.asarray(idx, dtype=np.uint64)
     t = np.asarray(t, dtype=np.uint64)
     seed = int(seed)
-    x0, x1, _, _ = philox4x32_10(t.astype(np.uint32) + np.zeros_like(idx, dtype=np.uint32),
-                                 (idx & MASK).astype(np.uint32),
-                                 (idx >> np.uint64(32)).astype(np.uint32),
-                                 np.uint32(stream) + np.zeros_like(idx, dtype=np.uint32),
-                                 seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    a = (x0 >> np.uint32(5)).astype(np.float64)
-    b = (x1 >> np.uint32(6)).astype(np.float64)
-    return (a * 67108864.0 + b) / 9007199254740992.0
+    j = idx >> np.uint64(1)
+    odd = (idx & np.uint64(1)).astype(bool)
+    x0, x1, x2, x3 = philox4x32_10(t.astype(np.uint32) + np.zeros_like(j, dtype=np.uint32),
+                                   (j & MASK).astype(np.uint32),
+                                   (j >> np.uint64(32)).astype(np.uint32),
+                                   np.uint32(stream) + np.zeros_like(j, dtype=np.uint32),
+                                   seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    a = np.where(odd, x2, x0) >> np.uint32(5)
+    b = np.where(odd, x3, x1) >> np.uint32(6)
+    return (a.astype(np.float64) * 67108864.0 + b.astype(np.float64)) / 9007199254740992.0
 
 
 def philox_u_source(seed, N, offset=0):
