@@ -51,6 +51,12 @@ class PanelModel(ctypes.Structure):
                 ("mrkv_hist", vp)]
 
 
+class PanelBatch(ctypes.Structure):
+    _fields_ = [("n_cal", ctypes.c_int32), ("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32),
+                ("n_lab", ctypes.c_int32), ("pol_pairs", vp), ("pol_index", vp), ("M_grid", vp), ("lab_level", vp),
+                ("lab_cdf", vp), ("mrkv_hist", vp)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "aiy_version": (ctypes.c_int32, []),
@@ -70,6 +76,10 @@ SIGNATURES = {
     "aiy_sim_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                              vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), vp]),
+    "aiy_sim_block_max_agents": (ctypes.c_int32, []),
+    "aiy_sim_block_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelBatch), vp, ctypes.c_int64, vp, vp, vp,
+                                               vp, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               vp, vp, vp, vp]),
     "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
     "aiy_index_ints_per_row": (ctypes.c_int32, []),
     "aiy_panel_index_ints_per_row": (ctypes.c_int32, []),

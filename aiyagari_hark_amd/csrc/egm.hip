@@ -436,16 +436,10 @@ extern "C" int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, 
   if (rc) return rc;
   rc = launch_build_index(h, m_next, rows, dims->n_a + 1, h->d_egm_idx, st);
   if (rc) return rc;
-  hipEvent_t e0, e1;
-  AIY_HIP(h, hipEventCreate(&e0));
-  AIY_HIP(h, hipEventCreate(&e1));
-  AIY_HIP(h, hipEventRecord(e0, st));
-  for (int k = 0; k < n_launch; ++k) launch_cycle(A, m_next, c_next, m_out, c_out, h->d_egm_idx, 0, nullptr, nullptr, 0.0, st);
-  AIY_HIP(h, hipEventRecord(e1, st));
-  AIY_HIP(h, hipEventSynchronize(e1));
-  AIY_HIP(h, hipEventElapsedTime(ms_out, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  int32_t trc = time_launches(
+      h, st, n_launch,
+      [&] { launch_cycle(A, m_next, c_next, m_out, c_out, h->d_egm_idx, 0, nullptr, nullptr, 0.0, st); }, ms_out);
+  if (trc) return trc;
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
 }

@@ -6,7 +6,9 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/aiyagari.h"
 
@@ -37,6 +39,10 @@ struct aiy_handle {
   unsigned long long* h_hdist = nullptr;
   double* h_K = nullptr;
   int* h_hlast = nullptr;
+  // block panel: per-calibration markets + seeds (device + pinned staging)
+  void* d_blk = nullptr;
+  void* h_blk = nullptr;
+  size_t blk_cap = 0;
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -67,5 +73,33 @@ inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
 #define AIY_CHECK_LAUNCH(h) AIY_HIP(h, hipGetLastError())
 
 inline hipStream_t as_stream(aiy_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Measurement hooks: n launches, each bracketed by its own pair of HIP events on `st`,
+// *ms = sum of the per-launch elapsed times (so inter-launch gaps are not charged to
+// the kernel; comparable with rocprofv3 --kernel-trace durations).
+template <class Launch>
+int32_t time_launches(aiy_handle* h, hipStream_t st, int n, Launch launch, float* ms) {
+  std::vector<hipEvent_t> ev(2 * (size_t)n, nullptr);
+  int32_t rc = AIY_OK;
+  for (auto& e : ev)
+    if (hipEventCreate(&e) != hipSuccess) { rc = fail(h, AIY_ERR_HIP, "hipEventCreate failed"); break; }
+  for (int k = 0; rc == AIY_OK && k < n; ++k) {
+    if (hipEventRecord(ev[2 * k], st) != hipSuccess) rc = fail(h, AIY_ERR_HIP, "hipEventRecord failed");
+    launch();
+    if (hipGetLastError() != hipSuccess) rc = fail(h, AIY_ERR_HIP, "kernel launch failed");
+    if (hipEventRecord(ev[2 * k + 1], st) != hipSuccess) rc = fail(h, AIY_ERR_HIP, "hipEventRecord failed");
+  }
+  if (rc == AIY_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(h, AIY_ERR_HIP, "hipStreamSynchronize failed");
+  float tot = 0.f;
+  for (int k = 0; rc == AIY_OK && k < n; ++k) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, ev[2 * k], ev[2 * k + 1]) != hipSuccess) rc = fail(h, AIY_ERR_HIP, "hipEventElapsedTime failed");
+    tot += t;
+  }
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (rc == AIY_OK) *ms = tot;
+  return rc;
+}
 
 }  // namespace aiy

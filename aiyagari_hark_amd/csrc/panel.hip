@@ -18,6 +18,7 @@
 // fixed order, so every bit of the history is reproducible run to run.
 #include "common.h"
 #include "internal.h"
+#include "panel_common.h"
 
 #include <algorithm>
 
@@ -64,58 +65,19 @@ struct PanelRun {
 __device__ __forceinline__ void mill(const aiy_market& mk, const int* mrkv_hist, long long n_total, double sum_a,
                                      double* sow, double* hist_A, double* hist_M) {
   const int t = (int)load_f64_agent(&sow[7]);
-  const double Aprev = sum_a / (double)n_total;   // np.mean(np.array(aNow))
-  const double AggK = Aprev;
-  const int Mrkv = mrkv_hist[t];
-  const double Prod = mk.prod[Mrkv ? 1 : 0];
-  const double AggL = mk.agg_L[Mrkv ? 1 : 0];
-  const double KtoL = AggK / AggL;
-  const double al = mk.cap_share;
-  const double Rnow = 1.0 + Prod * (al * pow(KtoL, al - 1.0)) - mk.depr_fac;
-  const double Wnow = Prod * ((1.0 - al) * pow(KtoL, al));
-  const double Mnow = Rnow * AggK + Wnow * AggL;
-  store_f64_agent(&sow[0], Mnow);
-  store_f64_agent(&sow[1], Aprev);
-  store_f64_agent(&sow[2], (double)Mrkv);
-  store_f64_agent(&sow[3], Rnow);
-  store_f64_agent(&sow[4], Wnow);
+  const Prices p = calc_prices(mk, mrkv_hist[t], sum_a / (double)n_total);   // np.mean(np.array(aNow))
+  store_f64_agent(&sow[0], p.Mnow);
+  store_f64_agent(&sow[1], p.Aprev);
+  store_f64_agent(&sow[2], (double)p.Mrkv);
+  store_f64_agent(&sow[3], p.Rnow);
+  store_f64_agent(&sow[4], p.Wnow);
   store_f64_agent(&sow[5], 0.0);  // Urate: everyone employed at UrateB = UrateG = 0
   store_f64_agent(&sow[7], (double)(t + 1));
-  if (hist_A) hist_A[t] = Aprev;
-  if (hist_M) hist_M[t] = Mnow;
+  if (hist_A) hist_A[t] = p.Aprev;
+  if (hist_M) hist_M[t] = p.Mnow;
 }
 
 // HARK LinearInterp at bracket i of an interleaved row (x0 = first node).
-// index_window with the row header (base, last bucket) already in registers.
-template <class I>
-__device__ __forceinline__ void index_window_hdr(const int* __restrict__ H, int base, int last, int n, double q, int& lo,
-                                                 int& hi) {
-  lo = 0;
-  hi = n;
-  if (base == kIdxNoBase) return;
-  const long long key = idx_key<I>(q) - (long long)base;
-  if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-  else if (key >= I::kBuckets - 1) {
-    if (last == I::kBuckets - 1) { lo = H[I::kBuckets - 1]; hi = n; } else { lo = n; hi = n; }
-  }
-  else if (key > last) { lo = n; hi = n; }
-  else { lo = H[key]; hi = H[key + 1]; }
-  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
-}
-
-__device__ __forceinline__ double lerp_pair(const double2* __restrict__ p, int i, double q, double x0) {
-  const double2 lo = p[i - 1], hi = p[i];
-  const double alpha = (q - lo.x) / (hi.x - lo.x);
-  const double v = (1.0 - alpha) * lo.y + alpha * hi.y;
-  return (q < x0) ? __builtin_nan("") : v;
-}
-
-constexpr int kLdsLab = 16;   // labour states (the KS form has S = 4 n_lab <= 64)
-constexpr int kPairs = 2;     // agent pairs per lane per pass
-constexpr int kAgents = 2 * kPairs;
-
-__device__ __forceinline__ double kBorrowNodeOf(const double2* p) { return p[0].x; }   // labour chains up to 16 states are staged in LDS
-
 __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, PanelRun r, aiy_market mk) {
   const double Mnow = load_f64_agent(&r.sow[0]);
   const int Mrkv = (int)load_f64_agent(&r.sow[2]);
@@ -458,20 +420,11 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
   r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 1;
   const int nb = sim_blocks(n_local);
-  hipEvent_t e0, e1;
-  AIY_HIP(h, hipEventCreate(&e0));
-  AIY_HIP(h, hipEventCreate(&e1));
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, 0);
-  AIY_HIP(h, hipEventRecord(e0, st));
-  for (int k = 0; k < n_launch; ++k)
-    hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, r, *mkt);
-  AIY_HIP(h, hipEventRecord(e1, st));
-  AIY_HIP(h, hipEventSynchronize(e1));
-  AIY_HIP(h, hipEventElapsedTime(ms_out, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   AIY_CHECK_LAUNCH(h);
-  return AIY_OK;
+  return time_launches(h, st, n_launch,
+                       [&] { hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, r, *mkt); },
+                       ms_out);
 }
 
 extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) {

@@ -86,7 +86,7 @@ class _Terminal:
 class AiyagariType:
     """AS:759-1415 on libaiyagari."""
 
-    def __init__(self, device=None, shock_mode="numpy", shock_seed=0, **kwds):
+    def __init__(self, device=None, shock_mode="numpy", shock_seed=0, panel_engine="auto", **kwds):
         params = init_Aiyagari_agents.copy()
         params.update(kwds)
         for k, v in params.items():
@@ -101,6 +101,7 @@ class AiyagariType:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.shock_mode = shock_mode
         self.shock_seed = shock_seed
+        self.panel_engine = panel_engine
         self.time_vary = []
         self.time_inv = ["DiscFac", "CRRA"]
         self.state_now = {"aNow": None, "mNow": None, "EmpNow": None, "LaborSupplyState": None}
@@ -152,15 +153,20 @@ class AiyagariType:
     def precompute_arrays(self):              # AS:906-1037
         if self.UrateB != 0.0 or self.UrateG != 0.0:
             raise NotImplementedError("UrateB/UrateG > 0 (full Krusell-Smith employment) is SURVEY §8f rank 2")
+        self.egm_batch = EgmBatch.from_numpy(*self.egm_arrays(), device=self.device)
+        self.add_to_time_inv("egm_batch")
+
+    def egm_arrays(self):
+        """Host inputs of solve_Aiyagari for the current AFunc: (aGrid, Mgrid, P, R_next,
+        W_next, M_next, lab, DiscFac, CRRA), precompute_arrays (AS:906-1037) reduced to
+        its unique [n_M, S] content."""
         S = 4 * self.LaborStatesNo
         R, W, M = sm.next_prices([f.intercept for f in self.AFunc], [f.slope for f in self.AFunc], self.Mgrid, S,
                                  self.UrateB, self.UrateG, self.LbrInd, self.ProdB, self.ProdG, self.CapShare,
                                  self.DeprFac)
         self.LSStates = sm.labor_levels(self.TauchenAux[0])
         lab = np.array([self.LSStates[sp // 4] for sp in range(S)])
-        self.egm_batch = EgmBatch.from_numpy(self.aGrid, self.Mgrid, self.MrkvIndArray, R, W, M, lab, self.DiscFac,
-                                             self.CRRA, device=self.device)
-        self.add_to_time_inv("egm_batch")
+        return self.aGrid, self.Mgrid, self.MrkvIndArray, R, W, M, lab, self.DiscFac, self.CRRA
 
     def solve(self, verbose=False):
         """[HARK] AgentType.solve -> solve_agent (cycles = 0: infinite horizon)."""
@@ -187,8 +193,9 @@ class AiyagariType:
         self.state_now["EmpNow"] = emp
         self.state_now["LaborSupplyState"] = lab
         self.t_sim = 0
-        if self.panel is None or self.panel.n_local != self.AgentCount or self.panel.act_T != self.T_sim:
-            self.panel = DevicePanel(self.AgentCount, device=self.device, act_T=self.T_sim)
+        if self.panel is None or self.panel.n_local != self.AgentCount or self.panel.act_T != self.T_sim \
+                or self.panel.engine != self.panel_engine:
+            self.panel = DevicePanel(self.AgentCount, device=self.device, act_T=self.T_sim, engine=self.panel_engine)
         self.lab_cdf = sm.choice_cdf_table(self.TauchenAux[1])          # agent's own chain (AS:1245, Q5)
 
     def market_action(self):                  # AS:1161
@@ -266,8 +273,7 @@ class AiyagariEconomy:
                                     sm.labor_levels(agent.TauchenAux[0]), dtype=torch.float64).to(agent.device)
         lab_cdf = torch.as_tensor(agent.lab_cdf, dtype=torch.float64).to(agent.device)
         hist = torch.as_tensor(np.asarray(self.MrkvNow_hist, dtype=np.int32)).to(agent.device)
-        market = dict(CapShare=self.CapShare, DeprFac=self.DeprFac, prod=(self.ProdB, self.ProdG),
-                      agg_L=((1.0 - self.UrateB) * self.LbrInd, (1.0 - self.UrateG) * self.LbrInd))
+        market = self.market_constants()
         p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, hist, market)
         p.reset(agent.kInit, agent.state_now["LaborSupplyState"], self.sow_init["Mnow"], self.sow_init["Aprev"],
                 self.sow_init["Mrkv"], self.sow_init["Rnow"], self.sow_init["Wnow"])
@@ -279,16 +285,23 @@ class AiyagariEconomy:
         else:
             p.run(0, self.act_T, shock_mode="philox", seed=agent.shock_seed, ge_iter=ge_iter)
         torch.cuda.synchronize(agent.device)
+        self.store_history(agent, p.sow_host(), p.a.cpu().numpy(), p.lab.cpu().numpy(), p.hist_A.cpu().numpy(),
+                           p.hist_M.cpu().numpy())
+
+    def market_constants(self):
+        """Constants of calc_R_and_W (AS:1867-1894) for the device mill."""
+        return dict(CapShare=self.CapShare, DeprFac=self.DeprFac, prod=(self.ProdB, self.ProdG),
+                    agg_L=((1.0 - self.UrateB) * self.LbrInd, (1.0 - self.UrateG) * self.LbrInd))
+
+    def store_history(self, agent, sow, aNow, lab, hist_A, hist_M):
+        """Write back one simulated history the way [HARK] Market.make_history leaves it."""
         self.Shk_idx = self.act_T
-        s = p.sow_host()
         for v in self.sow_vars:
-            self.sow_state[v] = s[v]
-        aNow = p.a.cpu().numpy()
+            self.sow_state[v] = sow[v]
         self.reap_state = {"aNow": [aNow], "EmpNow": [np.ones(agent.AgentCount)]}
         agent.state_now["aNow"] = aNow
-        agent.state_now["LaborSupplyState"] = p.lab.cpu().numpy().astype(np.int64)
-        self.history = {"Mrkv": list(np.asarray(self.MrkvNow_hist[:self.act_T])),
-                        "Aprev": p.hist_A.cpu().numpy(), "Mnow": p.hist_M.cpu().numpy(),
+        agent.state_now["LaborSupplyState"] = lab.astype(np.int64)
+        self.history = {"Mrkv": list(np.asarray(self.MrkvNow_hist[:self.act_T])), "Aprev": hist_A, "Mnow": hist_M,
                         "Urate": np.zeros(self.act_T)}
 
     def update_dynamics(self):                # [HARK] Market.update_dynamics

@@ -11,6 +11,15 @@ Shock sources (``u`` of get_shocks, Aiyagari_Support.py:1253-1254):
     before a solve makes the GPU history reproduce the reference's.
   * ``"philox"`` -- counter-based Philox4x32-10 on device (key = seed, counter =
     (GE iteration << 20 | t, global agent index)); independent of sharding.
+
+Two engines run the same per-period semantics:
+  * ``"grid"``  -- one launch per period over the whole population (aiy_sim_periods);
+    the engine for large panels (configs[1], configs[3]) and the only sharded one.
+  * ``"block"`` -- one workgroup per calibration with the agents resident in LDS for a
+    whole block of periods (aiy_sim_block_periods); the engine for the reference's own
+    350-700-agent panels, where a launch per period would be launch-bound.
+``"auto"`` picks ``block`` for unsharded panels of at most aiy_sim_block_max_agents().
+``BatchedPanel`` runs many calibrations' panels in one launch (Table II sweep).
 """
 from __future__ import annotations
 
@@ -26,8 +35,10 @@ F64 = torch.float64
 
 class DevicePanel:
     def __init__(self, n_local: int, device=None, agent_offset: int = 0, n_total: int | None = None,
-                 act_T: int = 11000):
+                 act_T: int = 11000, engine: str = "auto"):
         self.device = torch.device(device or "cuda")
+        if engine not in ("auto", "grid", "block"):
+            raise ValueError(f"engine {engine!r}")
         self.n_local = int(n_local)
         self.agent_offset = int(agent_offset)
         self.n_total = int(n_total if n_total is not None else n_local)
@@ -38,6 +49,13 @@ class DevicePanel:
         self.hist_A = torch.zeros(self.act_T, dtype=F64, device=self.device)
         self.hist_M = torch.zeros(self.act_T, dtype=F64, device=self.device)
         self._model = None
+        self.engine = engine
+
+    def _engine(self, h):
+        if self.engine != "auto":
+            return self.engine
+        small = self.n_local <= h.lib.aiy_sim_block_max_agents()
+        return "block" if small and self.n_total == self.n_local and self.agent_offset == 0 else "grid"
 
     def reset(self, a0, lab0, Mnow, Aprev, Mrkv, Rnow, Wnow):
         """sim_birth + Market.reset sow_init (Aiyagari_Support.py:1621-1628)."""
@@ -67,9 +85,11 @@ class DevicePanel:
         pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
                                                        ("pol_pairs", "pol_index", "M_grid", "lab_level", "lab_cdf",
                                                         "mrkv_hist")))
-        mk = _lib.Market(market["CapShare"], market["DeprFac"], (ctypes.c_double * 2)(*market["prod"]),
-                         (ctypes.c_double * 2)(*market["agg_L"]))
-        self._model = (pm, mk, keep)
+        mk = make_market(market)
+        pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
+                                                          ("pol_pairs", "pol_index", "M_grid", "lab_level", "lab_cdf",
+                                                           "mrkv_hist")))
+        self._model = (pm, mk, keep, pb)
 
     def run(self, t0: int, n_periods: int, shock_mode="philox", seed=0, ge_iter=0, u_host_source=None,
             chunk=1000, stream=None):
@@ -77,9 +97,16 @@ class DevicePanel:
         must return the next n x n_local uniforms (host)."""
         if self._model is None:
             raise RuntimeError("bind_model() first")
-        pm, mk, _ = self._model
+        pm, mk, _, pb = self._model
         h = _lib.handle(self.device.index)
         sp = _lib.stream_ptr(stream)
+        if self._engine(h) == "block":
+            if self.n_total != self.n_local or self.agent_offset != 0:
+                raise ValueError("the block engine does not shard agents")
+            seeds = (ctypes.c_uint64 * 1)(int(seed) & ((1 << 64) - 1))
+            run_block(h, pb, ctypes.byref(mk), self.n_local, self.a, self.lab, seeds, ge_iter, t0, n_periods,
+                      self.act_T, self.sow, self.hist_A, self.hist_M, shock_mode, u_host_source, chunk, sp, stream)
+            return
         if shock_mode == "philox":
             h.check(h.lib.aiy_sim_periods(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_local, self.agent_offset,
                                           self.n_total, _lib.ptr(self.a), _lib.ptr(self.lab), None, 0,
@@ -109,3 +136,102 @@ class DevicePanel:
         s = self.sow.cpu().numpy()
         return dict(Mnow=float(s[0]), Aprev=float(s[1]), Mrkv=int(s[2]), Rnow=float(s[3]), Wnow=float(s[4]),
                     Urate=float(s[5]))
+
+
+def make_market(market: dict) -> "_lib.Market":
+    return _lib.Market(market["CapShare"], market["DeprFac"], (ctypes.c_double * 2)(*market["prod"]),
+                       (ctypes.c_double * 2)(*market["agg_L"]))
+
+
+def run_block(h, pb, markets_ref, n_agents, a, lab, seeds, ge_iter, t0, n_periods, act_T, sow, hist_A, hist_M,
+              shock_mode, u_host_source, chunk, sp, stream):
+    """aiy_sim_block_periods over [t0, t0 + n_periods): Philox in one call, host uniforms
+    in chunks of ``chunk`` periods (u_host_source(n) -> [n_cal][n][n_agents] or, for one
+    calibration, [n][n_agents])."""
+    if shock_mode == "philox":
+        h.check(h.lib.aiy_sim_block_periods(h.h, ctypes.byref(pb), markets_ref, n_agents, _lib.ptr(a), _lib.ptr(lab),
+                                            None, seeds, int(ge_iter), int(t0), int(n_periods), int(act_T),
+                                            _lib.ptr(sow), _lib.ptr(hist_A), _lib.ptr(hist_M), sp),
+                "aiy_sim_block_periods")
+        return
+    if shock_mode != "numpy":
+        raise ValueError(shock_mode)
+    t, end = t0, t0 + n_periods
+    while t < end:
+        n = min(chunk, end - t)
+        u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
+        want = (pb.n_cal, n, n_agents)
+        if u.size != np.prod(want):
+            raise ValueError(f"u block shape {u.shape} != {want}")
+        ud = torch.from_numpy(u.reshape(want)).to(a.device)
+        h.check(h.lib.aiy_sim_block_periods(h.h, ctypes.byref(pb), markets_ref, n_agents, _lib.ptr(a), _lib.ptr(lab),
+                                            _lib.ptr(ud), seeds, int(ge_iter), int(t), int(n), int(act_T),
+                                            _lib.ptr(sow), _lib.ptr(hist_A), _lib.ptr(hist_M), sp),
+                "aiy_sim_block_periods")
+        torch.cuda.current_stream(a.device).synchronize() if stream is None else stream.synchronize()
+        del ud
+        t += n
+
+
+class BatchedPanel:
+    """Panels of n_cal independent calibrations (same S, n_M, n_a, n_lab and population
+    size), simulated together by the block engine: one launch covers every
+    calibration's periods.  Tensors are stacked over calibrations."""
+
+    def __init__(self, n_cal: int, n_agents: int, act_T: int, device=None):
+        self.device = torch.device(device or "cuda")
+        self.n_cal, self.n_agents, self.act_T = int(n_cal), int(n_agents), int(act_T)
+        self.a = torch.empty((n_cal, n_agents), dtype=F64, device=self.device)
+        self.lab = torch.empty((n_cal, n_agents), dtype=torch.uint8, device=self.device)
+        self.sow = torch.zeros((n_cal, _lib.AIY_SOW_DOUBLES), dtype=F64, device=self.device)
+        self.hist_A = torch.zeros((n_cal, act_T), dtype=F64, device=self.device)
+        self.hist_M = torch.zeros((n_cal, act_T), dtype=F64, device=self.device)
+        self._model = None
+
+    def reset(self, a0, lab0, sow0):
+        """a0 [n_cal] or [n_cal, n_agents]; lab0 [n_cal, n_agents]; sow0 [n_cal, 5]
+        (Mnow, Aprev, Mrkv, Rnow, Wnow)."""
+        a0 = np.asarray(a0, dtype=np.float64)
+        a0 = np.broadcast_to(a0[:, None] if a0.ndim == 1 else a0, (self.n_cal, self.n_agents))
+        self.a.copy_(torch.from_numpy(np.ascontiguousarray(a0)))
+        self.lab.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(lab0, dtype=np.uint8))))
+        sow = np.zeros((self.n_cal, _lib.AIY_SOW_DOUBLES))
+        sow[:, :5] = np.asarray(sow0, dtype=np.float64)
+        self.sow.copy_(torch.from_numpy(sow))
+        self.hist_A.zero_()
+        self.hist_M.zero_()
+
+    def bind_models(self, m_pol, c_pol, M_grid, lab_level, lab_cdf, mrkv_hist, markets):
+        """m_pol/c_pol [n_cal, S, n_M, n1] device; M_grid [n_cal, n_M]; lab_level
+        [n_cal, n_lab]; lab_cdf [n_cal, n_lab, n_lab]; mrkv_hist [n_cal, act_T];
+        markets: list of n_cal dicts (see make_market)."""
+        n_cal, S, n_M, n1 = m_pol.shape
+        if n_cal != self.n_cal:
+            raise ValueError("calibration count mismatch")
+        n_lab = int(lab_level.shape[1])
+        h = _lib.handle(self.device.index)
+        ipr = h.lib.aiy_panel_index_ints_per_row()
+        keep = dict(m_pol=m_pol.contiguous(), c_pol=c_pol.contiguous(), M_grid=M_grid.contiguous(),
+                    lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
+                    mrkv_hist=mrkv_hist.to(torch.int32).contiguous())
+        keep["pol_pairs"] = torch.empty((n_cal, S, n_M, n1, 2), dtype=F64, device=self.device)
+        keep["pol_index"] = torch.empty((n_cal * S * n_M, ipr), dtype=torch.int32, device=self.device)
+        h.check(h.lib.aiy_panel_prepare(h.h, n_cal * S * n_M, n1, _lib.ptr(keep["m_pol"]), _lib.ptr(keep["c_pol"]),
+                                        _lib.ptr(keep["pol_pairs"]), _lib.ptr(keep["pol_index"]), _lib.stream_ptr()),
+                "aiy_panel_prepare")
+        pb = _lib.PanelBatch(n_cal, S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
+                                                              ("pol_pairs", "pol_index", "M_grid", "lab_level",
+                                                               "lab_cdf", "mrkv_hist")))
+        mks = (_lib.Market * n_cal)(*(make_market(m) for m in markets))
+        self._model = (pb, mks, keep)
+
+    def run(self, t0, n_periods, shock_mode="philox", seeds=None, ge_iter=0, u_host_source=None, chunk=1000,
+            stream=None):
+        if self._model is None:
+            raise RuntimeError("bind_models() first")
+        pb, mks, _ = self._model
+        h = _lib.handle(self.device.index)
+        seeds = [0] * self.n_cal if seeds is None else list(seeds)
+        sd = (ctypes.c_uint64 * self.n_cal)(*(int(x) & ((1 << 64) - 1) for x in seeds))
+        run_block(h, pb, mks, self.n_agents, self.a, self.lab, sd, ge_iter, t0, n_periods, self.act_T, self.sow,
+                  self.hist_A, self.hist_M, shock_mode, u_host_source, chunk, _lib.stream_ptr(stream), stream)

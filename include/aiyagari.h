@@ -98,8 +98,9 @@ int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inp
                       aiy_stream stream);
 
 /* Measurement hook (bench.py): n_launch launches of the EGM cycle kernel alone from
- * (m_next, c_next) (search index built once, outside the timed region), bracketed by
- * HIP events on `stream`; *ms_out = elapsed milliseconds.  BLOCKING. */
+ * (m_next, c_next) (search index built once, outside the timed region), each bracketed
+ * by its own pair of HIP events on `stream`; *ms_out = sum of the per-launch elapsed
+ * milliseconds (gaps between launches excluded).  BLOCKING. */
 int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
                             const double* m_next, const double* c_next, double* m_out, double* c_out,
                             int32_t n_launch, float* ms_out, aiy_stream stream);
@@ -176,12 +177,46 @@ int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_m
                         int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
                         aiy_stream stream);
 
-/* Measurement hook (bench.py): n_launch back-to-back launches of the per-period panel
- * kernel (single rank, Philox shocks) bracketed by HIP events recorded on `stream`;
- * *ms_out = elapsed milliseconds.  Advances a/lab/sow like n_launch periods.  BLOCKING. */
+/* Measurement hook (bench.py): n_launch launches of the per-period panel kernel
+ * (single rank, Philox shocks), each bracketed by its own pair of HIP events on
+ * `stream`; *ms_out = sum of the per-launch elapsed milliseconds.  Advances a/lab/sow
+ * like n_launch periods.  BLOCKING. */
 int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                             int64_t n_local, double* a, uint8_t* lab, uint64_t seed, uint32_t ge_iter,
                             double* sow, int32_t n_launch, float* ms_out, aiy_stream stream);
+
+/* Batched small-population panel (Table II in the reference's Krusell-Smith mode: 350-700
+ * agents per calibration, act_T = 11 000; AH:217-249).  One workgroup owns one
+ * calibration: agents stay in registers for all n_periods, the per-period mean of `a`
+ * is a workgroup reduction and calc_R_and_W runs on lane 0 (no grid synchronisation),
+ * so a whole history is ONE launch.  Same per-period semantics as aiy_sim_periods.
+ * All calibrations share (S, n_M, n_a, n_lab); arrays are stacked over calibrations. */
+typedef struct {
+  int32_t n_cal, S, n_M, n_a, n_lab;
+  const double* pol_pairs;  /* [n_cal][S][n_M][n_a+1][2], aiy_panel_prepare */
+  const int32_t* pol_index; /* [n_cal][S][n_M][aiy_panel_index_ints_per_row()] */
+  const double* M_grid;     /* [n_cal][n_M] */
+  const double* lab_level;  /* [n_cal][n_lab] */
+  const double* lab_cdf;    /* [n_cal][n_lab][n_lab] */
+  const int32_t* mrkv_hist; /* [n_cal][act_T] */
+} aiy_panel_batch;
+
+/* Largest per-calibration population aiy_sim_block_periods accepts. */
+int32_t aiy_sim_block_max_agents(void);
+
+/* Periods t0 .. t0 + n_periods - 1 of every calibration's history.
+ *   markets, seeds: HOST arrays [n_cal]
+ *   a [n_cal][n_agents], lab [n_cal][n_agents] uint8 (device, in/out)
+ *   u: NULL -> Philox (counter (ge_iter<<20 | t, idx/2, 0), key seeds[c]), else host
+ *      uniforms [n_cal][n_periods][n_agents]
+ *   sow [n_cal][AIY_SOW_DOUBLES] (device, in/out); hist_A/hist_M [n_cal][act_T] or NULL.
+ * Asynchronous (the call waits for earlier work on `stream` before it refills its
+ * pinned staging buffer). */
+int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const aiy_market* markets,
+                              int64_t n_agents, double* a, uint8_t* lab, const double* u,
+                              const uint64_t* seeds, uint32_t ge_iter, int32_t t0, int32_t n_periods,
+                              int32_t act_T, double* sow, double* hist_A, double* hist_M,
+                              aiy_stream stream);
 
 /* Handle options. */
 #define AIY_OPT_USE_GRAPHS 1 /* value != 0: replay panel periods from a captured hipGraph */

@@ -53,6 +53,7 @@ def test_struct_layouts(lib):
     assert ctypes.sizeof(_lib.EgmInputs) == 9 * 8
     assert ctypes.sizeof(_lib.Market) == 6 * 8
     assert ctypes.sizeof(_lib.PanelModel) == 16 + 6 * 8
+    assert ctypes.sizeof(_lib.PanelBatch) == 24 + 6 * 8
 
 
 def test_argument_validation_without_gpu(lib):

@@ -116,9 +116,9 @@ def test_policy_eval_matches_oracle(gpu):
     assert rel_err(got[ok], want[ok]) == 0.0
 
 
-def _panel(gpu, fx, N, T):
+def _panel(gpu, fx, N, T, engine="grid"):
     from aiyagari_hark_amd.panel import DevicePanel
-    p = DevicePanel(N, device=gpu, act_T=T)
+    p = DevicePanel(N, device=gpu, act_T=T, engine=engine)
     m = torch.as_tensor(fx["m"]).to(gpu)
     c = torch.as_tensor(fx["c"]).to(gpu)
     p.bind_model(m, c, torch.as_tensor(fx["Mgrid"]).to(gpu), torch.as_tensor(fx["LSStates"]).to(gpu),
@@ -127,13 +127,14 @@ def _panel(gpu, fx, N, T):
     return p
 
 
-def test_panel_host_shocks_matches_golden(gpu):
+@pytest.mark.parametrize("engine", ["grid", "block"])
+def test_panel_host_shocks_matches_golden(gpu, engine):
     """50 periods x 350 agents with a committed uniform stream: labour states exact,
     assets and the K/M history to 1e-12 (summation order of the mean differs)."""
     fx = np.load(os.path.join(GOLD, "egm_cfg1.npz"))
     pf = np.load(os.path.join(GOLD, "panel_cfg1.npz"))
     N, T = 350, int(pf["T"])
-    p = _panel(gpu, fx, N, T)
+    p = _panel(gpu, fx, N, T, engine)
     p.reset(float(fx["KSS"]), pf["lab0"], float(fx["MSS"]), float(fx["KSS"]), 0, float(fx["RSS"]), float(fx["WSS"]))
     U = np.random.RandomState(int(pf["u_seed"])).random_sample((T, N))
     pos = {"t": 0}
@@ -151,11 +152,12 @@ def test_panel_host_shocks_matches_golden(gpu):
     assert rel_err(p.hist_M.cpu().numpy(), pf["hist_M"]) < 1e-12
 
 
-def test_panel_philox_stream_matches_oracle(gpu):
+@pytest.mark.parametrize("engine", ["grid", "block"])
+def test_panel_philox_stream_matches_oracle(gpu, engine):
     """Device Philox uniforms == oracle Philox: labour draws of 3 periods agree exactly."""
     fx = np.load(os.path.join(GOLD, "egm_cfg1.npz"))
     N, T, seed, offset = 7000, 3, 2024, 0
-    p = _panel(gpu, fx, N, T)
+    p = _panel(gpu, fx, N, T, engine)
     lab0 = np.repeat(np.arange(7), N // 7)
     p.reset(float(fx["KSS"]), lab0, float(fx["MSS"]), float(fx["KSS"]), 0, float(fx["RSS"]), float(fx["WSS"]))
     p.run(0, T, shock_mode="philox", seed=seed, ge_iter=1)
@@ -165,6 +167,68 @@ def test_panel_philox_stream_matches_oracle(gpu):
         u = PX.uniform((1 << 20) + t, np.arange(N, dtype=np.uint64), seed)
         lab = H.draw_labor(lab, u, fx["cdf"])
     assert np.array_equal(p.lab.cpu().numpy(), lab)
+
+
+def test_batched_panel_equals_single_panels(gpu):
+    """Three calibrations (different policies, shock seeds, odd population) in one block
+    launch == three single-calibration grid-engine histories: labour exact, assets and
+    the K/M history to 1e-12, final market state."""
+    from aiyagari_hark_amd.panel import BatchedPanel
+    names = ("egm_cfg1", "egm_cfg1_afunc2", "egm_ckpt")
+    fxs = [np.load(os.path.join(GOLD, n + ".npz")) for n in names]
+    N, T, seeds = 1001, 120, (5, 17, 99)
+    mk = dict(CapShare=0.36, DeprFac=0.08, prod=(1.0, 1.0), agg_L=(1.0, 1.0))
+    rng = np.random.default_rng(3)
+    lab0 = rng.integers(0, 7, (3, N))
+    bp = BatchedPanel(3, N, T, device=gpu)
+    dv = lambda x: torch.as_tensor(np.ascontiguousarray(x)).to(gpu)  # noqa: E731
+    bp.bind_models(dv(np.stack([f["m"] for f in fxs])), dv(np.stack([f["c"] for f in fxs])),
+                   dv(np.stack([f["Mgrid"] for f in fxs])), dv(np.stack([f["LSStates"] for f in fxs])),
+                   dv(np.stack([f["cdf"] for f in fxs])),
+                   dv(np.stack([f["Mrkv_hist"][:T].astype(np.int32) for f in fxs])), [mk] * 3)
+    bp.reset(np.array([float(f["KSS"]) for f in fxs]), lab0,
+             [[float(f["MSS"]), float(f["KSS"]), 0, float(f["RSS"]), float(f["WSS"])] for f in fxs])
+    bp.run(0, T // 2, shock_mode="philox", seeds=seeds, ge_iter=3)
+    bp.run(T // 2, T - T // 2, shock_mode="philox", seeds=seeds, ge_iter=3)
+    torch.cuda.synchronize()
+    for k, f in enumerate(fxs):
+        p = _panel(gpu, f, N, T, "grid")
+        p.reset(float(f["KSS"]), lab0[k], float(f["MSS"]), float(f["KSS"]), 0, float(f["RSS"]), float(f["WSS"]))
+        p.run(0, T, shock_mode="philox", seed=seeds[k], ge_iter=3)
+        torch.cuda.synchronize()
+        assert np.array_equal(bp.lab[k].cpu().numpy(), p.lab.cpu().numpy())
+        assert rel_err(bp.a[k].cpu().numpy(), p.a.cpu().numpy()) < 1e-12
+        assert rel_err(bp.hist_A[k].cpu().numpy(), p.hist_A.cpu().numpy()) < 1e-12
+        assert rel_err(bp.hist_M[k].cpu().numpy(), p.hist_M.cpu().numpy()) < 1e-12
+        assert rel_err(bp.sow[k, :5].cpu().numpy(), p.sow[:5].cpu().numpy()) < 1e-12
+
+
+def test_economy_batch_matches_oracle(gpu):
+    """Table II in the reference's algorithm: two calibrations solved to their KS fixed
+    point in one EconomyBatch (batched EGM + one block-panel launch per GE iteration)
+    reproduce each calibration's own oracle solve (numpy shock stream seeded per
+    economy): same GE iteration count, coefficients within 1e-9, r and K/Y within 1e-5."""
+    from aiyagari_hark_amd.sweep import EconomyBatch, build_economies
+    cells = [dict(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), dict(LaborAR=0.3, LaborSD=0.4, CRRA=3.0)]
+    econ_d = dict(act_T=1200, T_discard=400)
+    agent_d = dict(AgentCount=350)
+    econs = build_economies(cells, econ_d, agent_d, device=gpu, shock_mode="numpy", seed0=11)
+    eb = EconomyBatch(econs)
+    eb.solve()
+    got = eb.results()
+    for k, cell in enumerate(cells):
+        ref = H.KSModel(dict(econ_d, **cell), dict(agent_d, **cell))
+        log = []
+        ref.solve(H.numpy_global_u_source(11 + k, 350), log=log)
+        want = ref.results()
+        g = econs[k].ge_log
+        assert len(g) == len(log)
+        for a, o in zip(g, log):
+            assert a["cycles"] == o["cycles"]
+            assert np.allclose(a["intercept"], o["intercept"], rtol=1e-9, atol=1e-12)
+            assert np.allclose(a["slope"], o["slope"], rtol=1e-9, atol=1e-12)
+        assert abs(got[k]["r"] - want["r"]) < 1e-5
+        assert abs(got[k]["K_over_Y"] - want["saving_rate"] / 0.08) < 1e-5
 
 
 def test_ge_fixed_point_matches_oracle(gpu):
