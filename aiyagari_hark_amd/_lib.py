@@ -17,7 +17,8 @@ import threading
 import torch  # noqa: F401  (see module docstring: HIP runtime ordering)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libaiyagari.so")
+# AIYAGARI_LIB points at an alternative build of the same library (tuning experiments).
+LIB_PATH = os.environ.get("AIYAGARI_LIB") or os.path.join(HERE, "lib", "libaiyagari.so")
 
 AIY_OK = 0
 ERRORS = {-1: "AIY_ERR_ARG", -2: "AIY_ERR_HIP", -3: "AIY_ERR_STATE", -4: "AIY_ERR_UNSUPPORTED",
@@ -25,6 +26,8 @@ ERRORS = {-1: "AIY_ERR_ARG", -2: "AIY_ERR_HIP", -3: "AIY_ERR_STATE", -4: "AIY_ER
 AIY_MAX_STATES = 64
 AIY_SOW_DOUBLES = 8
 AIY_OPT_USE_GRAPHS = 1
+AIY_OPT_RESIDENT = 2
+AIY_OPT_RESIDENT_ORDER = 3
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

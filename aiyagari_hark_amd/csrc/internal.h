@@ -39,6 +39,11 @@ struct aiy_handle {
   unsigned long long* h_hdist = nullptr;
   double* h_K = nullptr;
   int* h_hlast = nullptr;
+  // resident panel: tagged partial-sum granules + timeout word; option
+  void* d_res_sync = nullptr;
+  bool use_resident = true;
+  int res_agents = 2;                // agents per lane per lookup pass (2 or 4)
+  int res_order = 0;                 // 0 slice order, 1 sorted by wealth, 2 sorted + rotated sweeps
   // block panel: per-calibration markets + seeds (device + pinned staging)
   void* d_blk = nullptr;
   void* h_blk = nullptr;

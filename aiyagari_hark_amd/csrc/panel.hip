@@ -34,16 +34,6 @@ constexpr int kTicketGroups = 16;
 constexpr int kTicketStride = 32;   // uints: 128 B apart
 constexpr int kGraphPeriods = 64;
 
-struct PanelDev {
-  int S, n_M, n_a, n_lab;
-  const double* M_grid;
-  const double* lab_level;
-  const double* lab_cdf;
-  const int* mrkv_hist;
-  const int* pol_index;     // PanelIdx rows (aiy_panel_prepare)
-  const double2* pol_pairs; // (m, c) interleaved rows (aiy_panel_prepare)
-};
-
 struct PanelRun {
   long long n, offset, n_total;
   double* a;
@@ -363,6 +353,14 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   r.hist_A = hist_A; r.hist_M = hist_M; r.finish = h->comm ? 0 : 1;
   const aiy_market mk = *mkt;
 
+  if (!h->comm && h->use_resident && n_local >= kResMinAgents && resident_supported(P)) {
+    // one persistent launch for the whole block of periods (panel_resident.hip)
+    hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
+    rc = launch_resident(h, P, mk, n_local, a, lab, u, u_ld, seed, ge_iter, t0, n_periods, sow, hist_A, hist_M, st);
+    if (rc) return rc;
+    AIY_CHECK_LAUNCH(h);
+    return resident_status(h, st);
+  }
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
   int done = 0;
   if (h->use_graphs && !h->comm && n_periods >= 2 * kGraphPeriods) {
@@ -422,6 +420,17 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   const int nb = sim_blocks(n_local);
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, 0);
   AIY_CHECK_LAUNCH(h);
+  if (h->use_resident && n_local >= kResMinAgents && resident_supported(P)) {
+    // one persistent launch of n_launch periods
+    rc = time_launches(h, st, 1,
+                       [&] {
+                         (void)launch_resident(h, P, *mkt, n_local, a, lab, nullptr, 0, seed, ge_iter, 0, n_launch, sow,
+                                               nullptr, nullptr, st);
+                       },
+                       ms_out);
+    if (rc) return rc;
+    return resident_status(h, st);
+  }
   return time_launches(h, st, n_launch,
                        [&] { hipLaunchKernelGGL(sim_period_kernel, dim3(nb), dim3(kSimBlock), 0, st, P, r, *mkt); },
                        ms_out);
@@ -431,6 +440,14 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
   if (!h) return AIY_ERR_ARG;
   switch (option) {
     case AIY_OPT_USE_GRAPHS: h->use_graphs = value != 0; return AIY_OK;
+    case AIY_OPT_RESIDENT:
+      h->use_resident = value != 0;
+      if (value == 2 || value == 4) h->res_agents = (int)value;
+      return AIY_OK;
+    case AIY_OPT_RESIDENT_ORDER:
+      if (value < 0 || value > 2) return fail(h, AIY_ERR_ARG, "AIY_OPT_RESIDENT_ORDER must be 0, 1 or 2");
+      h->res_order = (int)value;
+      return AIY_OK;
     default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
   }
 }

@@ -2,8 +2,20 @@
 #pragma once
 
 #include "common.h"
+#include "internal.h"
 
 namespace aiy {
+
+// One calibration's panel model on device (aiy_panel_model).
+struct PanelDev {
+  int S, n_M, n_a, n_lab;
+  const double* M_grid;
+  const double* lab_level;
+  const double* lab_cdf;
+  const int* mrkv_hist;
+  const int* pol_index;     // PanelIdx rows (aiy_panel_prepare)
+  const double2* pol_pairs; // (m, c) interleaved rows (aiy_panel_prepare)
+};
 
 // calc_R_and_W (AS:1839-1894) prices from aggregate capital K (= mean of a).
 struct Prices {
@@ -17,8 +29,12 @@ __device__ __forceinline__ Prices calc_prices(const aiy_market& mk, int Mrkv, do
   const double KtoL = AggK / AggL;
   const double al = mk.cap_share;
   Prices p;
-  p.Rnow = 1.0 + Prod * (al * pow(KtoL, al - 1.0)) - mk.depr_fac;
-  p.Wnow = Prod * ((1.0 - al) * pow(KtoL, al));
+  // KtoL ** al and KtoL ** (al - 1) from ONE log and ONE exp (the price update sits on
+  // every period's critical path; pow twice costs ~2x).  Differs from two pow calls by
+  // a few ulp.
+  const double ka = exp(al * log(KtoL));
+  p.Rnow = 1.0 + Prod * (al * (ka / KtoL)) - mk.depr_fac;
+  p.Wnow = Prod * ((1.0 - al) * ka);
   p.Mnow = p.Rnow * AggK + p.Wnow * AggL;
   p.Aprev = Aprev;
   p.Mrkv = Mrkv;
@@ -38,7 +54,12 @@ __device__ __forceinline__ void index_window_hdr(const int* __restrict__ H, int 
     if (last == I::kBuckets - 1) { lo = H[I::kBuckets - 1]; hi = n; } else { lo = n; hi = n; }
   }
   else if (key > last) { lo = n; hi = n; }
-  else { lo = H[key]; hi = H[key + 1]; }
+  else {
+    int2 w;   // H[key], H[key + 1] in ONE dword-aligned 8-byte load (one L1 access, not two)
+    __builtin_memcpy(&w, __builtin_assume_aligned(H + key, 4), sizeof(w));
+    lo = w.x;
+    hi = w.y;
+  }
   if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
 }
 
@@ -55,5 +76,12 @@ constexpr int kAgents = 2 * kPairs;
 
 __device__ __forceinline__ double kBorrowNodeOf(const double2* p) { return p[0].x; }
 
+// Persistent panel (panel_resident.hip), used by aiy_sim_periods on a single rank.
+int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, long long n, double* a, uint8_t* lab,
+                        const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
+                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st);
+int32_t resident_status(aiy_handle* h, hipStream_t st);
+bool resident_supported(const PanelDev& P);
+constexpr long long kResMinAgents = 65536;
 
 }  // namespace aiy

@@ -1,0 +1,567 @@
+// Persistent ("resident") Monte Carlo panel: a whole block of periods of
+// Market.make_history in ONE launch (same per-period
+// semantics as sim_period_kernel in panel.hip).
+//
+// Geometry: one 1024-thread workgroup per CU (grid = CU count, all resident; checked by
+// the cooperative launch), each owning a contiguous, even-aligned slice of the agents.
+// When the population fits (<= ~16k agents per CU, i.e. ~4M agents on MI355X) the
+// slice's assets and labour states live in LDS for the whole launch, so per period
+// the agents cost no HBM traffic at all; otherwise they stream from HBM (same code).
+//
+// One period, per workgroup:
+//   1. m = R a + W l, c = cFunc[4 l + 2 Mrkv + 1](m, M) (PanelIdx lookup), a = m - c,
+//      partial sum of a (fixed order);
+//   2. arrive: partial stored write-through (sc1), drained, counted on one of 8 group
+//      counters, the group's last arriver counts on the top counter (monotonic counts,
+//      no resets); the global last arriver sums the partials in fixed order, runs
+//      calc_R_and_W (AS:1867-1894), stores sow/history write-through and raises the
+//      period flag (MI355X_MICROARCH.md visibility, "sc1 payload + drained flag");
+//   3. while the last arriver works, everyone draws NEXT period's labour states
+//      (Philox + inverse CDF, AS:1253-1254): they do not depend on prices, so the
+//      draw hides behind the barrier;
+//   4. lane 0 polls the flag (relaxed, s_sleep, bounded by a wall-clock timeout) and
+//      reads the new prices with sc1 loads.
+// Every polled word is zeroed by a memset ahead of each launch; epochs are period
+// indices within the launch.  Partial sums are combined in fixed order, so histories
+// are reproducible run to run (they differ from the per-period kernel's only in the
+// summation order of the mean, ~1e-16 relative).
+#include "common.h"
+#include "internal.h"
+#include "panel_common.h"
+
+#include <algorithm>
+
+namespace aiy {
+
+constexpr int kResThreads = 1024;
+constexpr int kResMaxBlocks = 512;             // granule sweep: 16 granules per lane of one wave
+constexpr int kResGranPerLane = 2 * kResMaxBlocks / kWave;
+constexpr size_t kResLdsBudget = 150 * 1024;   // dynamic LDS per workgroup
+constexpr size_t kResHdrMaxBytes = 32 * 1024;  // row-header table in LDS
+constexpr unsigned long long kResTimeoutTicks = 400000000ull;  // 4 s of the 100 MHz wall clock
+constexpr size_t kResGranBytes = sizeof(unsigned long long) * 2 * 2 * kResMaxBlocks;
+constexpr size_t kResSyncBytes = kResGranBytes + 16;          // + timeout word, padded to 16 B
+
+// Row header of one policy row for the period loop: PanelIdx base and last bucket, and
+// the row's first node x0 (the NaN guard of HARK's LinearInterp below the grid).
+struct RowHdr {
+  int base, last;
+  double x0;
+};
+
+struct ResRun {
+  long long n, offset;       // local agents; global index of local agent 0 (Philox)
+  long long chunk;           // agents per workgroup (even)
+  double* a;
+  uint8_t* lab;
+  const double* u;           // host uniforms [n_periods][u_ld] from period t0, or nullptr
+  long long u_ld;
+  unsigned long long seed;
+  unsigned ge_iter;
+  int t0, n_periods;
+  double* sow;
+  unsigned long long* gran; // [2 parity][nb][2] tagged halves of the workgroup partials, zeroed
+  unsigned* tmo;            // timeout word, zeroed
+  double* hist_A;
+  double* hist_M;
+  int sort_len;             // SORT: power of two >= chunk
+  int rotate;               // start each workgroup's sweep at a different slice offset
+};
+
+__device__ __forceinline__ int draw_labour(const double* s_cdf, int n_lab, int l0, double u) {
+  int l = 0;
+  for (int q = 0; q < n_lab; ++q) l += (s_cdf[l0 * n_lab + q] <= u) ? 1 : 0;   // searchsorted(cdf, u, 'right')
+  return l;
+}
+
+// Labour states of period t for the slice (in place: lab(t-1) -> lab(t)).
+__device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long long start, int cnt, int t,
+                                           const double* s_cdf, int n_lab) {
+  const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
+  const double* u = r.u ? r.u + (size_t)(t - r.t0) * r.u_ld + start : nullptr;
+  for (int q = threadIdx.x; 2 * q < cnt; q += blockDim.x) {
+    const int i = 2 * q;
+    double u0, u1;
+    if (u) {
+      u0 = u[i];
+      u1 = i + 1 < cnt ? u[i + 1] : 0.0;
+    } else {
+#ifdef AIY_DIAG_NO_PHILOX
+      u0 = 0.37 + 1e-9 * (double)(i & 1023); u1 = 0.41 + 1e-9 * (double)(i & 1023);   // diagnostic build only
+#else
+      philox_uniform2(ctr0, (uint64_t)((r.offset + start + i) >> 1), r.seed, 0u, u0, u1);
+#endif
+    }
+    L[i] = (uint8_t)draw_labour(s_cdf, n_lab, L[i], u0);
+    if (i + 1 < cnt) L[i + 1] = (uint8_t)draw_labour(s_cdf, n_lab, L[i + 1], u1);
+  }
+}
+
+#ifdef AIY_POL_AUX
+// Experimental: policy gathers as buffer loads with cache-policy bits (aux: 1 sc0, 2 nt).
+typedef unsigned int aiy_v2u __attribute__((ext_vector_type(2)));
+typedef unsigned int aiy_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double2 buf_pair(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AIY_POL_AUX));
+}
+__device__ __forceinline__ double buf_x(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AIY_POL_AUX));
+}
+__device__ __forceinline__ int2 buf_i2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AIY_POL_AUX));
+}
+#endif
+
+constexpr int kResResort = 32;   // SORT: periods between re-sorts of a slice
+
+// Ascending bitonic sort of (A, perm) in LDS, n a power of two; ties by perm (stable
+// and reproducible).  Ends with a barrier.
+__device__ __forceinline__ void bitonic_sort(double* A, unsigned short* perm, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const double a0 = A[i], a1 = A[ixj];
+          const unsigned short p0 = perm[i], p1 = perm[ixj];
+          const bool gt = a0 > a1 || (a0 == a1 && p0 > p1);
+          if (((i & k) == 0) == gt) {
+            A[i] = a1; A[ixj] = a0;
+            perm[i] = p1; perm[ixj] = p0;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Dynamic LDS: [row headers (16-aligned)] [a: chunk doubles] [lab: chunk bytes]
+__host__ __device__ inline size_t res_hdr_bytes(int n_lab, int n_M) {
+  return ((size_t)n_lab * 2 * n_M * sizeof(RowHdr) + 15) / 16 * 16;
+}
+
+template <bool IN_LDS, int kResA, bool SORT>
+__global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
+  extern __shared__ __attribute__((aligned(16))) char s_dyn[];
+  __shared__ double s_cdf[kLdsLab * kLdsLab];
+  __shared__ double s_lvl[kLdsLab];
+  __shared__ double s_red[kResThreads / kWave];
+  __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
+  __shared__ int s_abort;         // sweep timeout
+
+  const int tid = threadIdx.x;
+  const int nthr = blockDim.x;
+  const int nb = gridDim.x;
+  const int n_M = P.n_M, n_a = P.n_a, n1 = n_a + 1, n_lab = P.n_lab;
+  const long long start = (long long)blockIdx.x * r.chunk;
+  const int cnt = (int)std::max(0LL, std::min(r.chunk, r.n - start));
+  RowHdr* hdr = reinterpret_cast<RowHdr*>(s_dyn);   // [(2 q + Mrkv) n_M + j]
+  double* A;
+  uint8_t* L;
+  unsigned short* perm = nullptr;    // SORT: agent (slice index) at sorted position k
+  const int P2 = SORT ? (int)r.sort_len : 0;
+  if constexpr (SORT) {
+    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_lab, n_M));
+    perm = reinterpret_cast<unsigned short*>(A + P2);
+    L = reinterpret_cast<uint8_t*>(perm + P2);
+  } else if constexpr (IN_LDS) {
+    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_lab, n_M));
+    L = reinterpret_cast<uint8_t*>(A + r.chunk);
+  } else {
+    A = r.a + start;
+    L = r.lab + start;
+  }
+  const int rot = r.rotate ? (int)(((long long)blockIdx.x * cnt) / nb) : 0;
+#ifdef AIY_POL_AUX
+  const __amdgpu_buffer_rsrc_t rpair = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)P.pol_pairs, (short)0, (int)((size_t)P.S * n_M * n1 * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)P.pol_index, (short)0, (int)((size_t)P.S * n_M * PanelIdx::kRow * 4), 0x00020000);
+#endif
+
+  for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = P.lab_cdf[q];
+  for (int q = tid; q < n_lab; q += nthr) s_lvl[q] = P.lab_level[q];
+  for (int q = tid; q < n_lab * 2 * n_M; q += nthr) {
+    const int j = q % n_M, qe = q / n_M;               // qe = 2 l + Mrkv
+    const int s = 4 * (qe >> 1) + 2 * (qe & 1) + 1;    // employed sub-state of labour l, aggregate Mrkv
+    const size_t row = (size_t)s * n_M + j;
+    const int* H = P.pol_index + row * PanelIdx::kRow;
+    hdr[q].base = H[PanelIdx::kBuckets + 1];
+    hdr[q].last = H[PanelIdx::kBuckets];
+    hdr[q].x0 = P.pol_pairs[row * n1].x;
+  }
+  if constexpr (SORT) {
+    for (int i = tid; i < P2; i += nthr) {
+      A[i] = i < cnt ? r.a[start + i] : __builtin_inf();
+      perm[i] = (unsigned short)i;
+      if (i < cnt) L[i] = r.lab[start + i];
+    }
+  } else if constexpr (IN_LDS) {
+    for (int i = tid; i < cnt; i += nthr) {
+      A[i] = r.a[start + i];
+      L[i] = r.lab[start + i];
+    }
+  }
+  if (tid == 0) {
+    s_price[0] = load_f64_agent(&r.sow[0]);
+    s_price[1] = load_f64_agent(&r.sow[3]);
+    s_price[2] = load_f64_agent(&r.sow[4]);
+    s_price[3] = load_f64_agent(&r.sow[2]);
+  }
+  __syncthreads();
+  draw_slice(r, L, start, cnt, r.t0, s_cdf, n_lab);
+
+  Prices last{};
+  for (int p = 0; p < r.n_periods; ++p) {
+    const int t = r.t0 + p;
+    if constexpr (SORT) {
+      if (p % kResResort == 0) {
+        __syncthreads();
+        bitonic_sort(A, perm, P2);   // agents by wealth: neighbouring lanes share policy lines
+      }
+    }
+    const double Mnow = s_price[0], Rnow = s_price[1], Wnow = s_price[2];
+    const int Mrkv = (int)s_price[3];
+    int j = 1;
+    double alpha = 0.0;
+    if (n_M > 1) {
+      j = lower_bound(P.M_grid, 0, n_M, Mnow);
+      j = j > n_M - 1 ? n_M - 1 : j;
+      j = j < 1 ? 1 : j;
+      alpha = (Mnow - P.M_grid[j - 1]) / (P.M_grid[j] - P.M_grid[j - 1]);
+    }
+    const int jlo = n_M > 1 ? j - 1 : 0, jhi = n_M > 1 ? j : 0;
+    __syncthreads();   // this period's labour draws complete
+
+    // ---- 1. agents: lookups, a = m - c, partial sum ----
+    double local = 0.0;
+    for (int g0 = tid * kResA; g0 < cnt; g0 += nthr * kResA) {
+      double m[kResA];
+      int ln[kResA];
+      int pos[kResA];
+#pragma unroll
+      for (int k = 0; k < kResA; ++k) {
+        int i = g0 + k < cnt ? g0 + k : cnt - 1;
+        if (rot) { i += rot; i = i >= cnt ? i - cnt : i; }
+        pos[k] = i;
+        ln[k] = SORT ? L[perm[i]] : L[i];
+        m[k] = Rnow * A[i] + Wnow * (s_lvl[ln[k]] * 1.0);                                   // AS:1283
+      }
+#ifdef AIY_DIAG_NO_LOOKUP
+#pragma unroll
+      for (int k = 0; k < kResA; ++k)
+        if (g0 + k < cnt) { A[pos[k]] = 0.9 * m[k]; local += 0.9 * m[k]; }   // diagnostic build only
+      continue;
+#endif
+      int lo[2 * kResA], hi[2 * kResA];
+      double x0[2 * kResA];
+#ifdef AIY_POL_AUX
+      unsigned ro[2 * kResA];   // byte offset of each row's pairs
+#pragma unroll
+      for (int k = 0; k < kResA; ++k) {
+        const int s = 4 * ln[k] + 2 * Mrkv + 1;                                             // employed (Urate = 0)
+        const unsigned r0 = (unsigned)s * n_M + jlo, r1 = (unsigned)s * n_M + jhi;
+        const RowHdr h0 = hdr[(2 * ln[k] + Mrkv) * n_M + jlo];
+        const RowHdr h1 = hdr[(2 * ln[k] + Mrkv) * n_M + jhi];
+        ro[2 * k] = r0 * (unsigned)n1 * 16u;
+        ro[2 * k + 1] = r1 * (unsigned)n1 * 16u;
+        x0[2 * k] = h0.x0;
+        x0[2 * k + 1] = h1.x0;
+        const RowHdr* hh[2] = {&h0, &h1};
+        const unsigned rr[2] = {r0, r1};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          int& l_ = lo[2 * k + e];
+          int& h_ = hi[2 * k + e];
+          l_ = 0; h_ = n_a;
+          const int base = hh[e]->base, lastb = hh[e]->last;
+          if (base != kIdxNoBase) {
+            const long long key = idx_key<PanelIdx>(m[k]) - (long long)base;
+            const int* H = P.pol_index + (size_t)rr[e] * PanelIdx::kRow;
+            if (!(m[k] > 0.0) || key < 0) { l_ = 0; h_ = H[0]; }
+            else if (key >= PanelIdx::kBuckets - 1) {
+              if (lastb == PanelIdx::kBuckets - 1) { l_ = H[PanelIdx::kBuckets - 1]; h_ = n_a; } else { l_ = n_a; h_ = n_a; }
+            } else if (key > lastb) { l_ = n_a; h_ = n_a; }
+            else {
+              const int2 w = buf_i2(ridx, (rr[e] * (unsigned)PanelIdx::kRow + (unsigned)key) * 4u);
+              l_ = w.x; h_ = w.y;
+            }
+            if (l_ < 0 || h_ > n_a || l_ > h_) { l_ = 0; h_ = n_a; }
+          }
+        }
+      }
+      bool more = true;
+      while (more) {
+        more = false;
+        double v[2 * kResA];
+        int mid[2 * kResA];
+#pragma unroll
+        for (int q = 0; q < 2 * kResA; ++q) {
+          mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
+          v[q] = lo[q] < hi[q] ? buf_x(rpair, ro[q] + (unsigned)mid[q] * 16u) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 2 * kResA; ++q) {
+          if (lo[q] < hi[q]) {
+            if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
+            more = more || (lo[q] < hi[q]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kResA; ++k) {
+        double f[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int b = lo[2 * k + e] < 1 ? 1 : lo[2 * k + e];
+          const double2 plo = buf_pair(rpair, ro[2 * k + e] + (unsigned)(b - 1) * 16u);
+          const double2 phi = buf_pair(rpair, ro[2 * k + e] + (unsigned)b * 16u);
+          const double al = (m[k] - plo.x) / (phi.x - plo.x);
+          const double v = (1.0 - al) * plo.y + al * phi.y;
+          f[e] = (m[k] < x0[2 * k + e]) ? __builtin_nan("") : v;
+        }
+        double c = f[0];
+        if (n_M > 1) c = (1 - alpha) * f[0] + alpha * f[1];                                  // LinearInterpOnInterp1D
+        if (g0 + k < cnt) {
+          const double an = m[k] - c;                                                       // AS:1415
+          A[pos[k]] = an;
+          local += an;
+        }
+      }
+    }
+
+#else
+      const double2* pr[2 * kResA];
+#pragma unroll
+      for (int k = 0; k < kResA; ++k) {
+        const int s = 4 * ln[k] + 2 * Mrkv + 1;                                             // employed (Urate = 0)
+        const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
+        const RowHdr h0 = hdr[(2 * ln[k] + Mrkv) * n_M + jlo];
+        const RowHdr h1 = hdr[(2 * ln[k] + Mrkv) * n_M + jhi];
+        pr[2 * k] = P.pol_pairs + r0 * n1;
+        pr[2 * k + 1] = P.pol_pairs + r1 * n1;
+        x0[2 * k] = h0.x0;
+        x0[2 * k + 1] = h1.x0;
+        index_window_hdr<PanelIdx>(P.pol_index + r0 * PanelIdx::kRow, h0.base, h0.last, n_a, m[k], lo[2 * k],
+                                   hi[2 * k]);
+        index_window_hdr<PanelIdx>(P.pol_index + r1 * PanelIdx::kRow, h1.base, h1.last, n_a, m[k], lo[2 * k + 1],
+                                   hi[2 * k + 1]);
+      }
+      bool more = true;
+      while (more) {
+        more = false;
+        double v[2 * kResA];
+        int mid[2 * kResA];
+#pragma unroll
+        for (int q = 0; q < 2 * kResA; ++q) {
+          mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
+          v[q] = lo[q] < hi[q] ? pr[q][mid[q]].x : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 2 * kResA; ++q) {
+          if (lo[q] < hi[q]) {
+            if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
+            more = more || (lo[q] < hi[q]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kResA; ++k) {
+        const int b0 = lo[2 * k] < 1 ? 1 : lo[2 * k];
+        const int b1 = lo[2 * k + 1] < 1 ? 1 : lo[2 * k + 1];
+        const double f0 = lerp_pair(pr[2 * k], b0, m[k], x0[2 * k]);
+        double c = f0;
+        if (n_M > 1) {
+          const double f1 = lerp_pair(pr[2 * k + 1], b1, m[k], x0[2 * k + 1]);
+          c = (1 - alpha) * f0 + alpha * f1;                                                // LinearInterpOnInterp1D
+        }
+        if (g0 + k < cnt) {
+          const double an = m[k] - c;                                                       // AS:1415
+          A[pos[k]] = an;
+          local += an;
+        }
+      }
+    }
+
+#endif
+    // ---- 2. publish the workgroup partial as two tagged granules ----
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
+    if ((tid & (kWave - 1)) == 0) s_red[tid / kWave] = local;
+    __syncthreads();
+    const unsigned e = (unsigned)p + 1;
+    unsigned long long* gslot = r.gran + (size_t)(p & 1) * 2 * nb;
+    if (tid == 0) {
+      double sb = 0.0;
+      for (int w = 0; w < nthr / kWave; ++w) sb += s_red[w];
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(sb);
+      __hip_atomic_store(&gslot[2 * blockIdx.x], ((unsigned long long)e << 32) | (bits >> 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gslot[2 * blockIdx.x + 1], ((unsigned long long)e << 32) | (bits & 0xffffffffull),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- 3. next period's labour draws overlap the exchange ----
+    if (p + 1 < r.n_periods) draw_slice(r, L, start, cnt, t + 1, s_cdf, n_lab);
+    // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices ----
+    if (tid < kWave) {
+      const int mrkv_next = P.mrkv_hist[t];
+      unsigned long long gv[kResGranPerLane];
+      const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+      int ok = 1;
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < kResGranPerLane; ++k) {
+          const int gi = tid * kResGranPerLane + k;
+          if (gi < 2 * nb) {
+            gv[k] = __hip_atomic_load(&gslot[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            all = all && (unsigned)(gv[k] >> 32) == e;
+          } else {
+            gv[k] = 0;
+          }
+        }
+        if (__all(all)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t_start > kResTimeoutTicks) { ok = 0; break; }
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kResGranPerLane; k += 2) {
+        const unsigned long long bits = ((gv[k] & 0xffffffffull) << 32) | (gv[k + 1] & 0xffffffffull);
+        acc += __longlong_as_double((long long)bits);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
+      if (tid == 0) {
+        if (!ok) __hip_atomic_store(r.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_abort = ok ? 0 : 1;
+        last = calc_prices(mk, mrkv_next, acc / (double)r.n);   // np.mean(np.array(aNow))
+        s_price[0] = last.Mnow;
+        s_price[1] = last.Rnow;
+        s_price[2] = last.Wnow;
+        s_price[3] = (double)last.Mrkv;
+        if (blockIdx.x == 0) {
+          if (r.hist_A) r.hist_A[t] = last.Aprev;
+          if (r.hist_M) r.hist_M[t] = last.Mnow;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_abort) return;   // sweep timeout: the host reports it (tmo word)
+  }
+  if constexpr (SORT) {
+    for (int k = tid; k < cnt; k += nthr) {
+      r.a[start + perm[k]] = A[k];
+      r.lab[start + k] = L[k];
+    }
+  } else if constexpr (IN_LDS) {
+    for (int i = tid; i < cnt; i += nthr) {
+      r.a[start + i] = A[i];
+      r.lab[start + i] = L[i];
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0 && r.n_periods > 0) {
+    r.sow[0] = last.Mnow;
+    r.sow[1] = last.Aprev;
+    r.sow[2] = (double)last.Mrkv;
+    r.sow[3] = last.Rnow;
+    r.sow[4] = last.Wnow;
+    r.sow[5] = 0.0;
+    r.sow[7] = (double)(r.t0 + r.n_periods);
+  }
+}
+
+struct ResGeometry {
+  int nb = 0;
+  long long chunk = 0;
+  bool in_lds = false;
+  size_t lds = 0;
+  int sort_len = 0;
+  bool can_sort = false;
+  size_t lds_sort = 0;
+};
+
+static ResGeometry res_geometry(aiy_handle* h, long long n, int n_lab, int n_M) {
+  ResGeometry G;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) cus = 1;
+  const long long want = (n + 4095) / 4096;          // >= ~4 agents per lane
+  G.nb = (int)std::max(1LL, std::min<long long>(std::min(cus, kResMaxBlocks), want));
+  G.chunk = (n + G.nb - 1) / G.nb;
+  G.chunk += G.chunk & 1;                            // even: Philox pairs never straddle workgroups
+  G.nb = (int)((n + G.chunk - 1) / G.chunk);
+  const size_t hdr = res_hdr_bytes(n_lab, n_M);
+  const size_t agents = (size_t)G.chunk * (sizeof(double) + 1);
+  G.in_lds = hdr + agents <= kResLdsBudget;
+  G.lds = G.in_lds ? (hdr + agents + 15) / 16 * 16 : hdr;
+  G.sort_len = 1;
+  while (G.sort_len < G.chunk) G.sort_len <<= 1;
+  const size_t sorted = hdr + (size_t)G.sort_len * (sizeof(double) + sizeof(unsigned short)) + G.chunk;
+  G.can_sort = G.sort_len <= 65536 && sorted <= kResLdsBudget;
+  G.lds_sort = (sorted + 15) / 16 * 16;
+  return G;
+}
+
+bool resident_supported(const PanelDev& P) { return res_hdr_bytes(P.n_lab, P.n_M) <= kResHdrMaxBytes; }
+
+static int32_t ensure_res_scratch(aiy_handle* h) {
+  if (!h->d_res_sync) {
+    AIY_HIP(h, hipMalloc((void**)&h->d_res_sync, kResSyncBytes));
+  }
+  return AIY_OK;
+}
+
+// Launch the resident kernel for periods [t0, t0 + n_periods) (single rank).
+int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, long long n, double* a, uint8_t* lab,
+                        const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
+                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
+  if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
+  const ResGeometry G = res_geometry(h, n, P.n_lab, P.n_M);
+  int32_t rc = ensure_res_scratch(h);
+  if (rc) return rc;
+  const void* kernels[3][2] = {
+      {reinterpret_cast<const void*>(sim_resident_kernel<false, 2, false>),
+       reinterpret_cast<const void*>(sim_resident_kernel<false, 4, false>)},
+      {reinterpret_cast<const void*>(sim_resident_kernel<true, 2, false>),
+       reinterpret_cast<const void*>(sim_resident_kernel<true, 4, false>)},
+      {reinterpret_cast<const void*>(sim_resident_kernel<true, 2, true>),
+       reinterpret_cast<const void*>(sim_resident_kernel<true, 4, true>)}};
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (auto& row : kernels)
+      for (const void* k : row)
+        AIY_HIP(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
+    attr_set = true;
+  }
+  ResRun r;
+  r.n = n; r.offset = 0; r.chunk = G.chunk; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld; r.seed = seed;
+  r.ge_iter = ge_iter; r.t0 = t0; r.n_periods = n_periods; r.sow = sow;
+  r.gran = reinterpret_cast<unsigned long long*>(h->d_res_sync);
+  r.tmo = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes);
+  r.hist_A = hist_A; r.hist_M = hist_M;
+  r.sort_len = G.sort_len; r.rotate = h->res_order == 2 ? 1 : 0;
+  PanelDev Pc = P;
+  aiy_market mkc = mk;
+  AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
+  void* args[] = {&Pc, &r, &mkc};
+  const bool sort = h->res_order > 0 && G.can_sort;
+  const int variant = sort ? 2 : (G.in_lds ? 1 : 0);
+  const void* fn = kernels[variant][h->res_agents == 4 ? 1 : 0];
+  AIY_HIP(h, hipLaunchCooperativeKernel(fn, dim3(G.nb), dim3(kResThreads), args,
+                                        (unsigned)(sort ? G.lds_sort : G.lds), st));
+  return AIY_OK;
+}
+
+// Timeout word of the last resident launch (0 = fine).  Synchronises `st`.
+int32_t resident_status(aiy_handle* h, hipStream_t st) {
+  if (!h->d_res_sync) return AIY_OK;
+  unsigned tmo = 0;
+  AIY_HIP(h, hipMemcpyAsync(&tmo, reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes, sizeof(unsigned),
+                            hipMemcpyDeviceToHost, st));
+  AIY_HIP(h, hipStreamSynchronize(st));
+  if (tmo) return fail(h, AIY_ERR_STATE, "resident panel: partial-sum exchange timed out (workgroups not co-resident?)");
+  return AIY_OK;
+}
+
+}  // namespace aiy

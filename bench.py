@@ -128,7 +128,7 @@ def panel_kernel_time(agent, econ, n_launch=200):
     a = p.a.clone()
     lab = p.lab.clone()
     sow = p.sow.clone()
-    pm, mk, _ = p._model
+    pm, mk = p._model[:2]
     ms = ctypes.c_float()
     stream = torch.cuda.current_stream()
     # warm

@@ -140,7 +140,8 @@ typedef struct {
   const double* M_grid;     /* [n_M]                                                       */
   const double* lab_level;  /* [n_lab] LSStates (AS:1265)                                  */
   const double* lab_cdf;    /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
-  const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805)                          */
+  const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805); must cover every period
+                               a call simulates (t0 + n_periods <= act_T)                    */
 } aiy_panel_model;
 
 /* Prepare a policy table [n_rows = S * n_M][n1] for the panel: interleave (m, c) into
@@ -169,18 +170,20 @@ int32_t aiy_panel_prepare(aiy_handle* h, int64_t n_rows, int32_t n1, const doubl
  *   agent_offset: global index of local agent 0 (Philox counter, sharding)
  * With a communicator bound (aiy_comm_init) the per-period sum of a is all-reduced
  * over RCCL before the prices are formed; otherwise n_local must equal n_total.
- * Asynchronous, except that with hipGraph replay enabled (default; single rank,
- * n_periods >= 128) the call returns after the replayed periods completed. */
+ * Asynchronous, except that the persistent path (AIY_OPT_RESIDENT) and hipGraph replay
+ * (single rank, n_periods >= 128) return after the periods completed. */
 int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                         int64_t n_local, int64_t agent_offset, int64_t n_total, double* a,
                         uint8_t* lab, const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter,
                         int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
                         aiy_stream stream);
 
-/* Measurement hook (bench.py): n_launch launches of the per-period panel kernel
- * (single rank, Philox shocks), each bracketed by its own pair of HIP events on
- * `stream`; *ms_out = sum of the per-launch elapsed milliseconds.  Advances a/lab/sow
- * like n_launch periods.  BLOCKING. */
+/* Measurement hook (bench.py): n_launch periods of the panel kernel (single rank,
+ * Philox shocks) -- n_launch per-period launches, each bracketed by its own pair of HIP
+ * events on `stream`, or with AIY_OPT_RESIDENT one persistent launch of n_launch periods
+ * between two events; *ms_out = kernel milliseconds for the n_launch periods.  Simulates
+ * periods 0 .. n_launch - 1 (mrkv_hist must hold n_launch entries) and advances a/lab/sow.
+ * BLOCKING. */
 int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                             int64_t n_local, double* a, uint8_t* lab, uint64_t seed, uint32_t ge_iter,
                             double* sow, int32_t n_launch, float* ms_out, aiy_stream stream);
@@ -220,6 +223,13 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 
 /* Handle options. */
 #define AIY_OPT_USE_GRAPHS 1 /* value != 0: replay panel periods from a captured hipGraph */
+#define AIY_OPT_RESIDENT 2   /* value != 0 (default): single-rank panels of >= 65536 agents run
+                                 a block of periods as ONE persistent launch (agents resident in
+                                 LDS, in-kernel exchange of partial sums per period); 0: one launch
+                                 per period; 2 or 4: persistent, with that many agents per lane */
+#define AIY_OPT_RESIDENT_ORDER 3 /* persistent panel sweep order: 0 slice order (default), 1 agents
+                                    re-sorted by wealth every 32 periods, 2 sorted + per-workgroup
+                                    rotated start (results equal up to the summation order) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

@@ -169,6 +169,64 @@ def test_panel_philox_stream_matches_oracle(gpu, engine):
     assert np.array_equal(p.lab.cpu().numpy(), lab)
 
 
+@pytest.mark.parametrize("mode,order", [("philox", 0), ("numpy", 0), ("philox", 1), ("philox", 2)])
+def test_resident_panel_equals_per_period_kernel(gpu, mode, order):
+    """The persistent panel (one launch, agents in LDS, in-kernel grid barrier) against
+    the one-launch-per-period kernel on 131 075 agents (odd: ragged last workgroup):
+    labour states exact, assets (relative to the panel's scale) / history / market state
+    to 1e-12 (the two differ only in the summation order of the mean); labour draws of the first periods against the
+    oracle Philox exactly."""
+    from aiyagari_hark_amd import _lib
+    fx = np.load(os.path.join(GOLD, "egm_cfg1.npz"))
+    N, T, seed = 131075, 150, 31
+    rng = np.random.default_rng(5)
+    lab0 = rng.integers(0, 7, N)
+    U = rng.random((T, N))
+    h = _lib.handle(gpu.index)
+    out = {}
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, order), "aiy_set_option")
+    for resident in (1, 0):
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, resident), "aiy_set_option")
+        try:
+            p = _panel(gpu, fx, N, T, "grid")
+            p.reset(float(fx["KSS"]), lab0, float(fx["MSS"]), float(fx["KSS"]), 0, float(fx["RSS"]),
+                    float(fx["WSS"]))
+            if mode == "philox":
+                p.run(0, 2, shock_mode="philox", seed=seed, ge_iter=2)
+                torch.cuda.synchronize()
+                out[(resident, "lab2")] = p.lab.cpu().numpy()
+                p.run(2, T - 2, shock_mode="philox", seed=seed, ge_iter=2)
+            else:
+                pos = {"t": 0}
+
+                def src(n):
+                    o = U[pos["t"]:pos["t"] + n]
+                    pos["t"] += n
+                    return o
+
+                p.run(0, T, shock_mode="numpy", u_host_source=src, chunk=64)
+            torch.cuda.synchronize()
+            out[resident] = (p.lab.cpu().numpy(), p.a.cpu().numpy(), p.hist_A.cpu().numpy(), p.hist_M.cpu().numpy(),
+                             p.sow.cpu().numpy())
+        finally:
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, 1), "aiy_set_option")
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, 0), "aiy_set_option")
+    res, ref = out[1], out[0]
+    assert np.array_equal(res[0], ref[0])
+    # assets near the borrowing limit come out of a cancellation (a = m - c), so they are
+    # compared relative to the panel's scale; the aggregates elementwise
+    assert np.max(np.abs(res[1] - ref[1])) / np.max(np.abs(ref[1])) < 1e-12
+    for x, y in zip(res[2:4], ref[2:4]):
+        assert rel_err(x, y) < 1e-12
+    assert rel_err(res[4][:5], ref[4][:5]) < 1e-12
+    assert res[4][7] == ref[4][7] == T
+    if mode == "philox":
+        lab = lab0.copy()
+        for t in range(2):
+            lab = H.draw_labor(lab, PX.uniform((2 << 20) + t, np.arange(N, dtype=np.uint64), seed), fx["cdf"])
+        assert np.array_equal(out[(1, "lab2")], lab)
+
+
 def test_batched_panel_equals_single_panels(gpu):
     """Three calibrations (different policies, shock seeds, odd population) in one block
     launch == three single-calibration grid-engine histories: labour exact, assets and
