@@ -1,0 +1,89 @@
+"""Panel-kernel tuning sweep (run on the GPU box): per-period time of the persistent
+panel at configs[1] size (N_a = 10 000, 1 000 006 agents) for every library build
+listed in $AIY_VARIANTS (name=path.so, comma separated; default: the in-tree build)
+and every (resident, agents-per-lane, order) option.  Each variant runs in its own
+child process (the library is loaded once per process).  Prints one JSON line per
+measurement."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib, opts):
+    sys.path.insert(0, ROOT)
+    if lib:
+        os.environ["AIYAGARI_LIB"] = lib
+    import ctypes
+    import numpy as np
+    import torch
+    from aiyagari_hark_amd import _lib, setup_math as sm
+    from aiyagari_hark_amd.egm import EgmBatch, egm_solve
+    from aiyagari_hark_amd.panel import DevicePanel
+    dev = torch.device("cuda:0")
+    n_a = int(os.environ.get("NA", 10000))
+    N = int(os.environ.get("NAG", 1000006))
+    T = int(os.environ.get("T", 400))
+    ss = sm.steady_state(1.0, 0.96, 0.08, 0.36, 1.0)
+    aG = sm.make_grid_exp_mult(0.001, 50.0, n_a, 2)
+    Mg = ss["MSS"] * sm.MGRID_BASE
+    agg, E = sm.employment_chain(8, 8, 2.5, 1.5, 0, 0, 0.75, 1.25)
+    y, P7 = sm.labor_tauchen(7, 0.6, 0.2)
+    P = sm.kron_states(P7, E)
+    R, W, M = sm.next_prices([0.35, 0.36], [0.8, 0.8], Mg, 28, 0, 0, 1, 1, 1, 0.36, 0.08)
+    lv = sm.labor_levels(y)
+    lab = np.array([lv[s // 4] for s in range(28)])
+    b = EgmBatch.from_numpy(aG, Mg, P, R, W, M, lab, 0.96, 1.0, device=dev)
+    m, c, cyc, d = egm_solve(b)
+    h = _lib.handle(0)
+    out = []
+    for (res, agents, order, presort, Tt) in opts:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res if res == 0 else agents), "opt")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, order), "opt")
+        p = DevicePanel(N, device=dev, act_T=T)
+        hist = torch.as_tensor(sm.markov_history(agg, T).astype(np.int32)).to(dev)
+        p.bind_model(m[0], c[0], b.M_grid[0], torch.as_tensor(lv).to(dev),
+                     torch.as_tensor(sm.choice_cdf_table(P7)).to(dev), hist,
+                     dict(CapShare=0.36, DeprFac=0.08, prod=(1.0, 1.0), agg_L=(1.0, 1.0)))
+        p.reset(ss["KSS"], np.repeat(np.arange(7), N // 7 + 1)[:N], ss["MSS"], ss["KSS"], 0, ss["RSS"], ss["WSS"])
+        # burn in to the ergodic wealth distribution, then time T periods
+        p.run(0, T, shock_mode="philox", seed=1)
+        torch.cuda.synchronize()
+        if presort:   # global wealth order (Philox keyed by position: timing experiment only)
+            key, perm = torch.sort(p.a)
+            p.a.copy_(key)
+            p.lab.copy_(p.lab[perm])
+            torch.cuda.synchronize()
+        pm, mk = p._model[:2]
+        ms = ctypes.c_float()
+        h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), N, _lib.ptr(p.a), _lib.ptr(p.lab),
+                                          3, 1, _lib.ptr(p.sow), Tt, ctypes.byref(ms),
+                                          torch.cuda.current_stream().cuda_stream), "time")
+        out.append(dict(lib=os.path.basename(lib or "default"), resident=res, agents=agents, order=order, presort=presort, T=Tt,
+                        us_per_period=1e3 * ms.value / Tt, K=float(p.a.mean())))
+        print(json.dumps(out[-1]), flush=True)
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--child":
+        lib = sys.argv[2] if sys.argv[2] != "-" else None
+        opts = json.loads(sys.argv[3])
+        child(lib, opts)
+        return
+    variants = os.environ.get("AIY_VARIANTS", "")
+    libs = [("default", None)] + [tuple(v.split("=", 1)) for v in variants.split(",") if v]
+    opts_all = [(1, 2, 0, 0, 400), (1, 4, 0, 0, 400), (1, 2, 1, 0, 400), (1, 2, 2, 0, 400), (0, 2, 0, 0, 400),
+                (1, 2, 0, 0, 50), (1, 2, 0, 1, 50), (1, 2, 0, 1, 10), (1, 2, 0, 1, 400)]
+    opts_var = [(1, 2, 0, 0, 400)]
+    for name, lib in libs:
+        opts = opts_all if lib is None else opts_var
+        rc = subprocess.run([sys.executable, __file__, "--child", lib or "-", json.dumps(opts)], timeout=300).returncode
+        if rc != 0:
+            print(json.dumps(dict(lib=name, error=rc)), flush=True)
+            sys.exit(rc)
+
+
+if __name__ == "__main__":
+    main()
