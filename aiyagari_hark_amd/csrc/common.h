@@ -122,9 +122,8 @@ __device__ __forceinline__ double interp_row(const double* __restrict__ x, const
 // rounding -- by a search over a handful of nodes.
 //   layout per row: H[0 .. BUCKETS - 1] (entries up to last + 1 valid),
 //   last = bucket of the last node at [BUCKETS], base at [BUCKETS + 1]
-// EgmIdx (256 / octave) is rebuilt every EGM cycle; PanelIdx (2048 / octave) is built
-// once per history and leaves ~1 node per bucket, so a panel lookup is one index line
-// plus one (x, c) pair line.
+// EgmIdx (256 / octave) is rebuilt every EGM cycle; the panel uses the finer bracket
+// index below (BrkIdx), built once per history.
 // ---------------------------------------------------------------------------------
 template <int SHIFT, int BUCKETS>
 struct IdxSpec {
@@ -133,7 +132,6 @@ struct IdxSpec {
   static constexpr int kRow = BUCKETS + 2;   // ints per row
 };
 using EgmIdx = IdxSpec<44, 16 * 256>;
-using PanelIdx = IdxSpec<41, 16 * 2048>;
 constexpr int kIdxShift = EgmIdx::kShift;
 constexpr int kIdxBuckets = EgmIdx::kBuckets;
 constexpr int kIdxRow = EgmIdx::kRow;
@@ -142,6 +140,69 @@ constexpr int kIdxNoBase = -2147483647 - 1;     // x[1] <= 0 or n < 2: index unu
 template <class I = EgmIdx>
 __device__ __forceinline__ long long idx_key(double q) {
   return (long long)(__double_as_longlong(q) >> I::kShift);
+}
+
+// ---------------------------------------------------------------------------------
+// Panel BRACKET index (aiy_panel_prepare, once per history).  Same log buckets
+// (4 096 per binary octave, 16 octaves above x[1]) but one 64-bit entry per bucket:
+//   bits 43..63  lo  = first i with key(x_i) >= bucket (= lower_bound of the edge)
+//   bits 40..42  cnt = nodes inside the bucket (saturated at 7)
+//   bits  0..39  low 40 bits of x[lo] (meaningful when cnt >= 1)
+// All doubles of one bucket share their top 24 bits, so for a query q in bucket b
+// with cnt == 1, x[lo] >= q  <=>  low40(x[lo]) >= low40(q): lower_bound is lo or
+// lo + 1, decided from the entry alone -- the panel lookup is then ONE index load
+// plus the (x, c) pair loads, with no dependent search step (cnt == 0 likewise).
+// Row layout (uint64): E[0 .. kBuckets - 1], E[kBuckets] = last bucket (int64),
+// E[kBuckets + 1] = base (int64).  The ABI passes the rows as int32 words (kRow).
+// ---------------------------------------------------------------------------------
+struct BrkIdx {
+  static constexpr int kShift = 40;
+  static constexpr int kBuckets = 16 * 4096;
+  static constexpr int kRowU64 = kBuckets + 2;
+  static constexpr int kRow = 2 * kRowU64;   // int32 words per row
+  static constexpr unsigned long long kLow = (1ull << 40) - 1;
+  static constexpr int kCntSat = 7;
+  static constexpr int kMaxNodes = 1 << 21;
+};
+using PanelIdx = BrkIdx;
+
+__host__ __device__ __forceinline__ unsigned long long brk_encode(int lo, int cnt, unsigned long long low) {
+  return ((unsigned long long)lo << 43) | ((unsigned long long)cnt << 40) | (low & BrkIdx::kLow);
+}
+__device__ __forceinline__ int brk_lo(unsigned long long e) { return (int)(e >> 43); }
+
+// Row header (base, last bucket) of a bracket-index row.
+__device__ __forceinline__ void brk_header(const int* __restrict__ row, int& base, int& last) {
+  const unsigned long long* E = reinterpret_cast<const unsigned long long*>(row);
+  last = (int)(long long)E[BrkIdx::kBuckets];
+  base = (int)(long long)E[BrkIdx::kBuckets + 1];
+}
+
+// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket-index row; lo == hi
+// means the bracket is already known (the common case).
+__device__ __forceinline__ void brk_window(const int* __restrict__ row, int base, int last, int n, double q, int& lo,
+                                           int& hi) {
+  const unsigned long long* E = reinterpret_cast<const unsigned long long*>(row);
+  lo = 0;
+  hi = n;
+  if (base == kIdxNoBase) return;
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
+  const long long key = (long long)(bits >> BrkIdx::kShift) - (long long)base;
+  if (!(q > 0.0) || key < 0) { lo = 0; hi = brk_lo(E[0]); }
+  else if (key >= BrkIdx::kBuckets - 1) {               // capped top bucket / beyond the span
+    if (last == BrkIdx::kBuckets - 1) { lo = brk_lo(E[BrkIdx::kBuckets - 1]); hi = n; } else { lo = n; hi = n; }
+  }
+  else if (key > last) { lo = n; hi = n; }              // above every node
+  else {
+    const unsigned long long e = E[key];
+    const int l = brk_lo(e);
+    const int c = (int)((e >> 40) & 7u);
+    if (c == 0) { lo = l; hi = l; }
+    else if (c == 1) { lo = l + (((e & BrkIdx::kLow) < (bits & BrkIdx::kLow)) ? 1 : 0); hi = lo; }
+    else if (c < BrkIdx::kCntSat) { lo = l; hi = l + c; }
+    else { lo = l; hi = brk_lo(E[key + 1]); }
+  }
+  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }  // defensive: unsorted rows
 }
 
 // Search window [lo, hi) of lower_bound(x[0..n), q) from the row index H (base given).

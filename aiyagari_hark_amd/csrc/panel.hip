@@ -101,10 +101,8 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
     const int s = 4 * q + 2 * Mrkv + 1;
     const int* h0 = P.pol_index + ((size_t)s * n_M + jlo) * PanelIdx::kRow;
     const int* h1 = P.pol_index + ((size_t)s * n_M + jhi) * PanelIdx::kRow;
-    s_base[2 * q] = h0[PanelIdx::kBuckets + 1];
-    s_base[2 * q + 1] = h1[PanelIdx::kBuckets + 1];
-    s_last[2 * q] = h0[PanelIdx::kBuckets];
-    s_last[2 * q + 1] = h1[PanelIdx::kBuckets];
+    brk_header(h0, s_base[2 * q], s_last[2 * q]);
+    brk_header(h1, s_base[2 * q + 1], s_last[2 * q + 1]);
   }
   __syncthreads();
   double local = 0.0;
@@ -174,13 +172,15 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
       const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
       pr[2 * k] = P.pol_pairs + r0 * n1;
       pr[2 * k + 1] = P.pol_pairs + r1 * n1;
-      index_window_hdr<PanelIdx>(P.pol_index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
+      panel_window(P.pol_index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
                                  lo[2 * k], hi[2 * k]);
-      index_window_hdr<PanelIdx>(P.pol_index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
+      panel_window(P.pol_index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
                                  m[k], lo[2 * k + 1], hi[2 * k + 1]);
     }
     // lock-step bracket searches of all 2 kAgents rows (windows hold ~1 node)
-    bool more = true;
+    bool more = false;
+#pragma unroll
+    for (int q = 0; q < 2 * kAgents; ++q) more = more || (lo[q] < hi[q]);
     while (more) {
       more = false;
       double v[2 * kAgents];

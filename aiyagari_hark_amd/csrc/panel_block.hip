@@ -109,10 +109,8 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
       const int s = 4 * q + 2 * Mrkv + 1;
       const int* h0 = index + ((size_t)s * n_M + jlo) * PanelIdx::kRow;
       const int* h1 = index + ((size_t)s * n_M + jhi) * PanelIdx::kRow;
-      s_base[2 * q] = h0[PanelIdx::kBuckets + 1];
-      s_base[2 * q + 1] = h1[PanelIdx::kBuckets + 1];
-      s_last[2 * q] = h0[PanelIdx::kBuckets];
-      s_last[2 * q + 1] = h1[PanelIdx::kBuckets];
+      brk_header(h0, s_base[2 * q], s_last[2 * q]);
+      brk_header(h1, s_base[2 * q + 1], s_last[2 * q + 1]);
     }
     __syncthreads();
     const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
@@ -151,12 +149,14 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
         const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
         pr[2 * k] = pairs + r0 * n1;
         pr[2 * k + 1] = pairs + r1 * n1;
-        index_window_hdr<PanelIdx>(index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
+        panel_window(index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
                                    lo[2 * k], hi[2 * k]);
-        index_window_hdr<PanelIdx>(index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
+        panel_window(index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
                                    m[k], lo[2 * k + 1], hi[2 * k + 1]);
       }
-      bool more = true;
+      bool more = false;
+#pragma unroll
+      for (int q = 0; q < 2 * A; ++q) more = more || (lo[q] < hi[q]);
       while (more) {
         more = false;
         double v[2 * A];

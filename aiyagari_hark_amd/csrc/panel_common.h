@@ -13,7 +13,7 @@ struct PanelDev {
   const double* lab_level;
   const double* lab_cdf;
   const int* mrkv_hist;
-  const int* pol_index;     // PanelIdx rows (aiy_panel_prepare)
+  const int* pol_index;     // BrkIdx rows (aiy_panel_prepare), int32 words
   const double2* pol_pairs; // (m, c) interleaved rows (aiy_panel_prepare)
 };
 
@@ -41,26 +41,11 @@ __device__ __forceinline__ Prices calc_prices(const aiy_market& mk, int Mrkv, do
   return p;
 }
 
-// index_window with the row header (base, last bucket) already in registers.
-template <class I>
-__device__ __forceinline__ void index_window_hdr(const int* __restrict__ H, int base, int last, int n, double q, int& lo,
-                                                 int& hi) {
-  lo = 0;
-  hi = n;
-  if (base == kIdxNoBase) return;
-  const long long key = idx_key<I>(q) - (long long)base;
-  if (!(q > 0.0) || key < 0) { lo = 0; hi = H[0]; }
-  else if (key >= I::kBuckets - 1) {
-    if (last == I::kBuckets - 1) { lo = H[I::kBuckets - 1]; hi = n; } else { lo = n; hi = n; }
-  }
-  else if (key > last) { lo = n; hi = n; }
-  else {
-    int2 w;   // H[key], H[key + 1] in ONE dword-aligned 8-byte load (one L1 access, not two)
-    __builtin_memcpy(&w, __builtin_assume_aligned(H + key, 4), sizeof(w));
-    lo = w.x;
-    hi = w.y;
-  }
-  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }
+// Bracket-index window of one policy row with its header (base, last bucket) already in
+// registers (brk_window, common.h).
+__device__ __forceinline__ void panel_window(const int* __restrict__ row, int base, int last, int n, double q, int& lo,
+                                             int& hi) {
+  brk_window(row, base, last, n, q, lo, hi);
 }
 
 __device__ __forceinline__ double lerp_pair(const double2* __restrict__ p, int i, double q, double x0) {

@@ -9,7 +9,7 @@
 // the agents cost no HBM traffic at all; otherwise they stream from HBM (same code).
 //
 // One period, per workgroup:
-//   1. m = R a + W l, c = cFunc[4 l + 2 Mrkv + 1](m, M) (PanelIdx lookup), a = m - c,
+//   1. m = R a + W l, c = cFunc[4 l + 2 Mrkv + 1](m, M) (bracket-index lookup), a = m - c,
 //      partial sum of a (fixed order);
 //   2. arrive: partial stored write-through (sc1), drained, counted on one of 8 group
 //      counters, the group's last arriver counts on the top counter (monotonic counts,
@@ -42,7 +42,7 @@ constexpr unsigned long long kResTimeoutTicks = 400000000ull;  // 4 s of the 100
 constexpr size_t kResGranBytes = sizeof(unsigned long long) * 2 * 2 * kResMaxBlocks;
 constexpr size_t kResSyncBytes = kResGranBytes + 16;          // + timeout word, padded to 16 B
 
-// Row header of one policy row for the period loop: PanelIdx base and last bucket, and
+// Row header of one policy row for the period loop: bracket-index base and last bucket, and
 // the row's first node x0 (the NaN guard of HARK's LinearInterp below the grid).
 struct RowHdr {
   int base, last;
@@ -97,20 +97,6 @@ __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long lon
   }
 }
 
-#ifdef AIY_POL_AUX
-// Experimental: policy gathers as buffer loads with cache-policy bits (aux: 1 sc0, 2 nt).
-typedef unsigned int aiy_v2u __attribute__((ext_vector_type(2)));
-typedef unsigned int aiy_v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ double2 buf_pair(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AIY_POL_AUX));
-}
-__device__ __forceinline__ double buf_x(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AIY_POL_AUX));
-}
-__device__ __forceinline__ int2 buf_i2(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AIY_POL_AUX));
-}
-#endif
 
 constexpr int kResResort = 32;   // SORT: periods between re-sorts of a slice
 
@@ -173,12 +159,6 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     L = r.lab + start;
   }
   const int rot = r.rotate ? (int)(((long long)blockIdx.x * cnt) / nb) : 0;
-#ifdef AIY_POL_AUX
-  const __amdgpu_buffer_rsrc_t rpair = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)P.pol_pairs, (short)0, (int)((size_t)P.S * n_M * n1 * 16), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)P.pol_index, (short)0, (int)((size_t)P.S * n_M * PanelIdx::kRow * 4), 0x00020000);
-#endif
 
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = P.lab_cdf[q];
   for (int q = tid; q < n_lab; q += nthr) s_lvl[q] = P.lab_level[q];
@@ -186,9 +166,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     const int j = q % n_M, qe = q / n_M;               // qe = 2 l + Mrkv
     const int s = 4 * (qe >> 1) + 2 * (qe & 1) + 1;    // employed sub-state of labour l, aggregate Mrkv
     const size_t row = (size_t)s * n_M + j;
-    const int* H = P.pol_index + row * PanelIdx::kRow;
-    hdr[q].base = H[PanelIdx::kBuckets + 1];
-    hdr[q].last = H[PanelIdx::kBuckets];
+    brk_header(P.pol_index + row * PanelIdx::kRow, hdr[q].base, hdr[q].last);
     hdr[q].x0 = P.pol_pairs[row * n1].x;
   }
   if constexpr (SORT) {
@@ -213,6 +191,12 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
   draw_slice(r, L, start, cnt, r.t0, s_cdf, n_lab);
 
   Prices last{};
+#ifdef AIY_DIAG_PHASES
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = 0;
+#define AIY_PH(k) do { if (tid == 0) { const unsigned long long tn = __builtin_amdgcn_s_memrealtime(); if (k) ph[k - 1] += tn - tq; tq = tn; } } while (0)
+#else
+#define AIY_PH(k) do {} while (0)
+#endif
   for (int p = 0; p < r.n_periods; ++p) {
     const int t = r.t0 + p;
     if constexpr (SORT) {
@@ -233,6 +217,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     }
     const int jlo = n_M > 1 ? j - 1 : 0, jhi = n_M > 1 ? j : 0;
     __syncthreads();   // this period's labour draws complete
+    AIY_PH(0);
 
     // ---- 1. agents: lookups, a = m - c, partial sum ----
     double local = 0.0;
@@ -256,82 +241,6 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
 #endif
       int lo[2 * kResA], hi[2 * kResA];
       double x0[2 * kResA];
-#ifdef AIY_POL_AUX
-      unsigned ro[2 * kResA];   // byte offset of each row's pairs
-#pragma unroll
-      for (int k = 0; k < kResA; ++k) {
-        const int s = 4 * ln[k] + 2 * Mrkv + 1;                                             // employed (Urate = 0)
-        const unsigned r0 = (unsigned)s * n_M + jlo, r1 = (unsigned)s * n_M + jhi;
-        const RowHdr h0 = hdr[(2 * ln[k] + Mrkv) * n_M + jlo];
-        const RowHdr h1 = hdr[(2 * ln[k] + Mrkv) * n_M + jhi];
-        ro[2 * k] = r0 * (unsigned)n1 * 16u;
-        ro[2 * k + 1] = r1 * (unsigned)n1 * 16u;
-        x0[2 * k] = h0.x0;
-        x0[2 * k + 1] = h1.x0;
-        const RowHdr* hh[2] = {&h0, &h1};
-        const unsigned rr[2] = {r0, r1};
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          int& l_ = lo[2 * k + e];
-          int& h_ = hi[2 * k + e];
-          l_ = 0; h_ = n_a;
-          const int base = hh[e]->base, lastb = hh[e]->last;
-          if (base != kIdxNoBase) {
-            const long long key = idx_key<PanelIdx>(m[k]) - (long long)base;
-            const int* H = P.pol_index + (size_t)rr[e] * PanelIdx::kRow;
-            if (!(m[k] > 0.0) || key < 0) { l_ = 0; h_ = H[0]; }
-            else if (key >= PanelIdx::kBuckets - 1) {
-              if (lastb == PanelIdx::kBuckets - 1) { l_ = H[PanelIdx::kBuckets - 1]; h_ = n_a; } else { l_ = n_a; h_ = n_a; }
-            } else if (key > lastb) { l_ = n_a; h_ = n_a; }
-            else {
-              const int2 w = buf_i2(ridx, (rr[e] * (unsigned)PanelIdx::kRow + (unsigned)key) * 4u);
-              l_ = w.x; h_ = w.y;
-            }
-            if (l_ < 0 || h_ > n_a || l_ > h_) { l_ = 0; h_ = n_a; }
-          }
-        }
-      }
-      bool more = true;
-      while (more) {
-        more = false;
-        double v[2 * kResA];
-        int mid[2 * kResA];
-#pragma unroll
-        for (int q = 0; q < 2 * kResA; ++q) {
-          mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
-          v[q] = lo[q] < hi[q] ? buf_x(rpair, ro[q] + (unsigned)mid[q] * 16u) : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < 2 * kResA; ++q) {
-          if (lo[q] < hi[q]) {
-            if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
-            more = more || (lo[q] < hi[q]);
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kResA; ++k) {
-        double f[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int b = lo[2 * k + e] < 1 ? 1 : lo[2 * k + e];
-          const double2 plo = buf_pair(rpair, ro[2 * k + e] + (unsigned)(b - 1) * 16u);
-          const double2 phi = buf_pair(rpair, ro[2 * k + e] + (unsigned)b * 16u);
-          const double al = (m[k] - plo.x) / (phi.x - plo.x);
-          const double v = (1.0 - al) * plo.y + al * phi.y;
-          f[e] = (m[k] < x0[2 * k + e]) ? __builtin_nan("") : v;
-        }
-        double c = f[0];
-        if (n_M > 1) c = (1 - alpha) * f[0] + alpha * f[1];                                  // LinearInterpOnInterp1D
-        if (g0 + k < cnt) {
-          const double an = m[k] - c;                                                       // AS:1415
-          A[pos[k]] = an;
-          local += an;
-        }
-      }
-    }
-
-#else
       const double2* pr[2 * kResA];
 #pragma unroll
       for (int k = 0; k < kResA; ++k) {
@@ -343,12 +252,14 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
         pr[2 * k + 1] = P.pol_pairs + r1 * n1;
         x0[2 * k] = h0.x0;
         x0[2 * k + 1] = h1.x0;
-        index_window_hdr<PanelIdx>(P.pol_index + r0 * PanelIdx::kRow, h0.base, h0.last, n_a, m[k], lo[2 * k],
+        panel_window(P.pol_index + r0 * PanelIdx::kRow, h0.base, h0.last, n_a, m[k], lo[2 * k],
                                    hi[2 * k]);
-        index_window_hdr<PanelIdx>(P.pol_index + r1 * PanelIdx::kRow, h1.base, h1.last, n_a, m[k], lo[2 * k + 1],
+        panel_window(P.pol_index + r1 * PanelIdx::kRow, h1.base, h1.last, n_a, m[k], lo[2 * k + 1],
                                    hi[2 * k + 1]);
       }
-      bool more = true;
+      bool more = false;
+#pragma unroll
+      for (int q = 0; q < 2 * kResA; ++q) more = more || (lo[q] < hi[q]);
       while (more) {
         more = false;
         double v[2 * kResA];
@@ -384,12 +295,12 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
       }
     }
 
-#endif
     // ---- 2. publish the workgroup partial as two tagged granules ----
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
     if ((tid & (kWave - 1)) == 0) s_red[tid / kWave] = local;
     __syncthreads();
+    AIY_PH(1);
     const unsigned e = (unsigned)p + 1;
     unsigned long long* gslot = r.gran + (size_t)(p & 1) * 2 * nb;
     if (tid == 0) {
@@ -403,6 +314,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     }
     // ---- 3. next period's labour draws overlap the exchange ----
     if (p + 1 < r.n_periods) draw_slice(r, L, start, cnt, t + 1, s_cdf, n_lab);
+    AIY_PH(2);
     // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices ----
     if (tid < kWave) {
       const int mrkv_next = P.mrkv_hist[t];
@@ -425,6 +337,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t_start > kResTimeoutTicks) { ok = 0; break; }
       }
+      AIY_PH(3);
       double acc = 0.0;
 #pragma unroll
       for (int k = 0; k < kResGranPerLane; k += 2) {
@@ -449,6 +362,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     }
     __syncthreads();
     if (s_abort) return;   // sweep timeout: the host reports it (tmo word)
+    AIY_PH(4);
   }
   if constexpr (SORT) {
     for (int k = tid; k < cnt; k += nthr) {
@@ -461,6 +375,12 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
       r.lab[start + i] = L[i];
     }
   }
+#ifdef AIY_DIAG_PHASES
+  if (tid == 0 && (blockIdx.x == 0 || blockIdx.x == nb / 2 || blockIdx.x == nb - 1))
+    printf("[phases] block %d/%d cnt %d: lookup %.2f publish+draw %.2f sweep %.2f tail %.2f us/period\n", blockIdx.x, nb,
+           cnt, ph[0] * 0.01 / r.n_periods, ph[1] * 0.01 / r.n_periods, ph[2] * 0.01 / r.n_periods,
+           ph[3] * 0.01 / r.n_periods);
+#endif
   if (blockIdx.x == 0 && tid == 0 && r.n_periods > 0) {
     r.sow[0] = last.Mnow;
     r.sow[1] = last.Aprev;

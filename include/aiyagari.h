@@ -145,9 +145,11 @@ typedef struct {
 } aiy_panel_model;
 
 /* Prepare a policy table [n_rows = S * n_M][n1] for the panel: interleave (m, c) into
- * pairs [n_rows][n1][2] and build a fine log-bucket search index of every row (about one
- * node per bucket, so a panel lookup touches one index line and one pair line).
- * Asynchronous. */
+ * pairs [n_rows][n1][2] and build the bracket index of every row: 4 096 log buckets per
+ * binary octave, one 64-bit entry per bucket holding the lower_bound of the bucket edge,
+ * the number of nodes in the bucket and the low bits of its first node, so a panel
+ * lookup is one index load plus the bracketing pair loads, with no search step when the
+ * bucket holds at most one node.  n1 <= 2^21.  Asynchronous. */
 int32_t aiy_panel_index_ints_per_row(void);
 int32_t aiy_panel_prepare(aiy_handle* h, int64_t n_rows, int32_t n1, const double* m_pol,
                           const double* c_pol, double* pairs, int32_t* index, aiy_stream stream);

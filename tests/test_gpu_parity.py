@@ -349,6 +349,68 @@ def test_search_index_equals_binary_search(gpu):
             assert H[r, b] == np.searchsorted(xr, edge), (r, b)
 
 
+def _brk_bracket(E, n, q, shift=40, n_buckets=16 * 4096):
+    """Host restatement of brk_window (csrc/common.h) on one bracket-index row E
+    (uint64): the lower_bound of q over x[0..n), or (lo, hi) when a search remains."""
+    last, base = int(np.int64(E[n_buckets])), int(np.int64(E[n_buckets + 1]))
+    bits = int(np.float64(q).view(np.uint64))
+    key = (bits >> shift) - base
+    lo_of = lambda e: int(e) >> 43  # noqa: E731
+    if not q > 0 or key < 0:
+        return 0, lo_of(E[0])
+    if key >= n_buckets - 1:
+        return (lo_of(E[n_buckets - 1]), n) if last == n_buckets - 1 else (n, n)
+    if key > last:
+        return n, n
+    e = int(E[key])
+    lo, cnt, low = lo_of(e), (e >> 40) & 7, e & ((1 << 40) - 1)
+    if cnt == 0:
+        return lo, lo
+    if cnt == 1:
+        i = lo + (1 if low < (bits & ((1 << 40) - 1)) else 0)
+        return i, i
+    return (lo, lo + cnt) if cnt < 7 else (lo, lo_of(E[key + 1]))
+
+
+def test_panel_bracket_index_semantics(gpu):
+    """aiy_panel_prepare's bracket index: for queries across the whole row (nodes
+    themselves, their neighbours in ulps, random values, below / above the grid) the
+    decoded window always contains numpy's searchsorted(x[:-1], q) and is a single
+    point whenever the bucket holds at most one node."""
+    from aiyagari_hark_amd import _lib
+    fx = np.load(os.path.join(GOLD, "egm_cfg1_afunc2.npz"))
+    m = np.ascontiguousarray(fx["m"][:3, :2])          # 6 rows of 33 nodes
+    rng = np.random.default_rng(2)
+    big = np.sort(np.concatenate([[1e-7], np.cumsum(rng.exponential(0.004, 3000)) + 0.3]))
+    rows = [r for r in m.reshape(-1, m.shape[-1])] + [big[: m.shape[-1]]]
+    n1 = m.shape[-1]
+    X = np.stack(rows)
+    h = _lib.handle(gpu.index)
+    ipr = h.lib.aiy_panel_index_ints_per_row()
+    dm = torch.as_tensor(X).to(gpu)
+    dc = torch.as_tensor(X * 0.5).to(gpu)
+    pairs = torch.empty((X.shape[0], n1, 2), dtype=torch.float64, device=gpu)
+    idx = torch.empty((X.shape[0], ipr), dtype=torch.int32, device=gpu)
+    h.check(h.lib.aiy_panel_prepare(h.h, X.shape[0], n1, _lib.ptr(dm), _lib.ptr(dc), _lib.ptr(pairs), _lib.ptr(idx),
+                                    _lib.stream_ptr()), "aiy_panel_prepare")
+    torch.cuda.synchronize()
+    assert np.array_equal(pairs.cpu().numpy()[..., 0], X)
+    E_all = idx.cpu().numpy().view(np.uint64)
+    resolved = 0
+    for r, x in enumerate(X):
+        E = E_all[r]
+        xs = x[:-1]
+        n = len(xs)
+        qs = [xs, np.nextafter(xs, np.inf), np.nextafter(xs, -np.inf), rng.uniform(0, 1.2 * x[-1], 400),
+              np.array([-1.0, 0.0, 1e-9, 1e-7, x[-1] * 3, 1e6])]
+        for q in np.concatenate(qs):
+            want = int(np.searchsorted(xs, q))
+            lo, hi = _brk_bracket(E, n, float(q))
+            assert lo <= want <= hi, (r, q, lo, hi, want)
+            resolved += lo == hi
+    assert resolved > 0
+
+
 def test_stationary_capital_supply_matches_oracle(gpu):
     """E1/E2 at r = 4 %: stationary EGM tables bit-exact (CRRA 1), Young-lottery K to 1e-10."""
     from aiyagari_hark_amd.stationary import Calibration, StationaryBatch

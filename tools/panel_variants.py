@@ -39,9 +39,30 @@ def child(lib, opts):
     m, c, cyc, d = egm_solve(b)
     h = _lib.handle(0)
     out = []
+    bench_panel = None
+    if os.environ.get("BENCH_REGIME"):
+        # the bench's own economy after one GE solve (act_T = 2000): its converged policy
+        # and end-of-history population
+        sys.path.insert(0, ROOT)
+        import bench
+        econ, agent = bench.make_economy(seed=0, n_agents=N, n_a=n_a, act_T=2000, device=dev, t_discard=500)
+        bench.run_step(econ, agent, bench.Probe())
+        bench_panel = agent.panel
     for (res, agents, order, presort, Tt) in opts:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res if res == 0 else agents), "opt")
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, order), "opt")
+        if bench_panel is not None:
+            p = bench_panel
+            a0, l0, s0 = p.a.clone(), p.lab.clone(), p.sow.clone()
+            pm, mk = p._model[:2]
+            ms = ctypes.c_float()
+            h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), N, _lib.ptr(a0), _lib.ptr(l0),
+                                              99, 7, _lib.ptr(s0), Tt, ctypes.byref(ms),
+                                              torch.cuda.current_stream().cuda_stream), "time")
+            out.append(dict(lib=os.path.basename(lib or "default"), regime="bench", resident=res, agents=agents,
+                            order=order, T=Tt, us_per_period=1e3 * ms.value / Tt, K=float(a0.mean())))
+            print(json.dumps(out[-1]), flush=True)
+            continue
         p = DevicePanel(N, device=dev, act_T=T)
         hist = torch.as_tensor(sm.markov_history(agg, T).astype(np.int32)).to(dev)
         p.bind_model(m[0], c[0], b.M_grid[0], torch.as_tensor(lv).to(dev),
