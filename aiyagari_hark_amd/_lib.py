@@ -50,14 +50,13 @@ class Market(ctypes.Structure):
 
 class PanelModel(ctypes.Structure):
     _fields_ = [("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32), ("n_lab", ctypes.c_int32),
-                ("pol_pairs", vp), ("pol_index", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
-                ("mrkv_hist", vp)]
+                ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp), ("mrkv_hist", vp)]
 
 
 class PanelBatch(ctypes.Structure):
     _fields_ = [("n_cal", ctypes.c_int32), ("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32),
-                ("n_lab", ctypes.c_int32), ("pol_pairs", vp), ("pol_index", vp), ("M_grid", vp), ("lab_level", vp),
-                ("lab_cdf", vp), ("mrkv_hist", vp)]
+                ("n_lab", ctypes.c_int32), ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
+                ("mrkv_hist", vp)]
 
 
 # name -> (restype, argtypes)
@@ -85,8 +84,9 @@ SIGNATURES = {
                                                vp, vp, vp, vp]),
     "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
     "aiy_index_ints_per_row": (ctypes.c_int32, []),
-    "aiy_panel_index_ints_per_row": (ctypes.c_int32, []),
-    "aiy_panel_prepare": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp, vp]),
+    "aiy_panel_table_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "aiy_panel_build": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, vp, vp, vp, vp]),
     "aiy_build_index": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]),
     "aiy_comm_unique_id": (ctypes.c_int32, [vp]),
     "aiy_comm_init": (ctypes.c_int32, [vp, vp, ctypes.c_int32, ctypes.c_int32]),

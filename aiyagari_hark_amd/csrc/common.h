@@ -143,54 +143,43 @@ __device__ __forceinline__ long long idx_key(double q) {
 }
 
 // ---------------------------------------------------------------------------------
-// Panel BRACKET index (aiy_panel_prepare, once per history).  Same log buckets
-// (4 096 per binary octave, 16 octaves above x[1]) but one 64-bit entry per bucket:
+// BRACKET index (the panel's merged policy tables, panel_common.h): log buckets of a
+// sorted positive node list -- 2^(52 - shift) per binary octave, `buckets` in all,
+// starting at a base node -- with one 64-bit entry per bucket:
 //   bits 43..63  lo  = first i with key(x_i) >= bucket (= lower_bound of the edge)
 //   bits 40..42  cnt = nodes inside the bucket (saturated at 7)
-//   bits  0..39  low 40 bits of x[lo] (meaningful when cnt >= 1)
-// All doubles of one bucket share their top 24 bits, so for a query q in bucket b
-// with cnt == 1, x[lo] >= q  <=>  low40(x[lo]) >= low40(q): lower_bound is lo or
-// lo + 1, decided from the entry alone -- the panel lookup is then ONE index load
-// plus the (x, c) pair loads, with no dependent search step (cnt == 0 likewise).
-// Row layout (uint64): E[0 .. kBuckets - 1], E[kBuckets] = last bucket (int64),
-// E[kBuckets + 1] = base (int64).  The ABI passes the rows as int32 words (kRow).
+//   bits  0..39  bits [t, t + 40) of x[lo], t = max(shift - 40, 0) (cnt >= 1)
+// All doubles of one bucket share their bits above `shift`, so for a query q in bucket
+// b with cnt == 1 the stored bits decide x[lo] < q (lower_bound = lo + 1) or x[lo] >= q
+// (lo) from the entry alone -- a lookup is ONE index load with no dependent search step
+// (cnt == 0 likewise); only a tie in the stored bits (t > 0) or cnt >= 2 leaves a
+// short search.  Layout (uint64): E[0 .. buckets - 1], E[buckets] = last bucket,
+// E[buckets + 1] = base key (int64).
 // ---------------------------------------------------------------------------------
 struct BrkIdx {
-  static constexpr int kShift = 40;
-  static constexpr int kBuckets = 16 * 4096;
-  static constexpr int kRowU64 = kBuckets + 2;
-  static constexpr int kRow = 2 * kRowU64;   // int32 words per row
   static constexpr unsigned long long kLow = (1ull << 40) - 1;
   static constexpr int kCntSat = 7;
   static constexpr int kMaxNodes = 1 << 21;
 };
-using PanelIdx = BrkIdx;
 
 __host__ __device__ __forceinline__ unsigned long long brk_encode(int lo, int cnt, unsigned long long low) {
   return ((unsigned long long)lo << 43) | ((unsigned long long)cnt << 40) | (low & BrkIdx::kLow);
 }
+__host__ __device__ __forceinline__ int brk_low_shift(int shift) { return shift > 40 ? shift - 40 : 0; }
 __device__ __forceinline__ int brk_lo(unsigned long long e) { return (int)(e >> 43); }
 
-// Row header (base, last bucket) of a bracket-index row.
-__device__ __forceinline__ void brk_header(const int* __restrict__ row, int& base, int& last) {
-  const unsigned long long* E = reinterpret_cast<const unsigned long long*>(row);
-  last = (int)(long long)E[BrkIdx::kBuckets];
-  base = (int)(long long)E[BrkIdx::kBuckets + 1];
-}
-
-// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket-index row; lo == hi
+// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket index; lo == hi
 // means the bracket is already known (the common case).
-__device__ __forceinline__ void brk_window(const int* __restrict__ row, int base, int last, int n, double q, int& lo,
-                                           int& hi) {
-  const unsigned long long* E = reinterpret_cast<const unsigned long long*>(row);
+__device__ __forceinline__ void brk_window(const unsigned long long* __restrict__ E, int shift, int buckets, int base,
+                                           int last, int n, double q, int& lo, int& hi) {
   lo = 0;
   hi = n;
   if (base == kIdxNoBase) return;
   const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
-  const long long key = (long long)(bits >> BrkIdx::kShift) - (long long)base;
+  const long long key = (long long)(bits >> shift) - (long long)base;
   if (!(q > 0.0) || key < 0) { lo = 0; hi = brk_lo(E[0]); }
-  else if (key >= BrkIdx::kBuckets - 1) {               // capped top bucket / beyond the span
-    if (last == BrkIdx::kBuckets - 1) { lo = brk_lo(E[BrkIdx::kBuckets - 1]); hi = n; } else { lo = n; hi = n; }
+  else if (key >= buckets - 1) {                        // capped top bucket / beyond the span
+    if (last == buckets - 1) { lo = brk_lo(E[buckets - 1]); hi = n; } else { lo = n; hi = n; }
   }
   else if (key > last) { lo = n; hi = n; }              // above every node
   else {
@@ -198,7 +187,13 @@ __device__ __forceinline__ void brk_window(const int* __restrict__ row, int base
     const int l = brk_lo(e);
     const int c = (int)((e >> 40) & 7u);
     if (c == 0) { lo = l; hi = l; }
-    else if (c == 1) { lo = l + (((e & BrkIdx::kLow) < (bits & BrkIdx::kLow)) ? 1 : 0); hi = lo; }
+    else if (c == 1) {
+      const int t = brk_low_shift(shift);
+      const unsigned long long xs = e & BrkIdx::kLow, qs = (bits >> t) & BrkIdx::kLow;
+      if (xs != qs) { lo = l + (xs < qs ? 1 : 0); hi = lo; }   // x[l] < q  <=>  lower_bound = l + 1
+      else if (t == 0) { lo = l; hi = l; }                      // q == x[l]
+      else { lo = l; hi = l + 1; }                              // tie in the stored bits: one step
+    }
     else if (c < BrkIdx::kCntSat) { lo = l; hi = l + c; }
     else { lo = l; hi = brk_lo(E[key + 1]); }
   }

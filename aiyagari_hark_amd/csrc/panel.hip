@@ -67,7 +67,6 @@ __device__ __forceinline__ void mill(const aiy_market& mk, const int* mrkv_hist,
   if (hist_M) hist_M[t] = p.Mnow;
 }
 
-// HARK LinearInterp at bracket i of an interleaved row (x0 = first node).
 __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, PanelRun r, aiy_market mk) {
   const double Mnow = load_f64_agent(&r.sow[0]);
   const int Mrkv = (int)load_f64_agent(&r.sow[2]);
@@ -76,33 +75,20 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
   const int t = (int)load_f64_agent(&r.sow[7]);
   const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
   const double* u = r.u ? r.u + (size_t)(t - r.u_t0) * r.u_ld : nullptr;
-  const int n_M = P.n_M, n_a = P.n_a, n1 = n_a + 1, n_lab = P.n_lab;
+  const int n_M = P.n_M, n_lab = P.n_lab, n_J = P.tab.g.n_J;
   // LinearInterpOnInterp1D bracket in M: the same for every agent of the period.
-  int j = 1;
-  double alpha = 0.0;
-  if (n_M > 1) {
-    j = lower_bound(P.M_grid, 0, n_M, Mnow);
-    j = j > n_M - 1 ? n_M - 1 : j;
-    j = j < 1 ? 1 : j;
-    alpha = (Mnow - P.M_grid[j - 1]) / (P.M_grid[j] - P.M_grid[j - 1]);
-  }
-  const int jlo = n_M > 1 ? j - 1 : 0;
-  const int jhi = n_M > 1 ? j : 0;
-  // Stage the labour chain (inverse CDF rows, levels) and the index headers (base,
-  // last bucket) of this period's rows in LDS: the per-agent dependent chain then has
-  // no global hop before the policy lookup.
+  int jc;
+  double alpha;
+  m_bracket(P.M_grid, n_M, Mnow, jc, alpha);
+  // Stage the labour chain (inverse CDF rows, levels) and the period's cell headers in
+  // LDS: the per-agent dependent chain then has no global hop before the policy lookup.
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
-  __shared__ int s_base[2 * kLdsLab];
-  __shared__ int s_last[2 * kLdsLab];
+  __shared__ CellHdr s_hdr[kLdsLab];
   for (int q = threadIdx.x; q < n_lab * n_lab; q += blockDim.x) s_cdf[q] = P.lab_cdf[q];
   for (int q = threadIdx.x; q < n_lab; q += blockDim.x) {
     s_lvl[q] = P.lab_level[q];
-    const int s = 4 * q + 2 * Mrkv + 1;
-    const int* h0 = P.pol_index + ((size_t)s * n_M + jlo) * PanelIdx::kRow;
-    const int* h1 = P.pol_index + ((size_t)s * n_M + jhi) * PanelIdx::kRow;
-    brk_header(h0, s_base[2 * q], s_last[2 * q]);
-    brk_header(h1, s_base[2 * q + 1], s_last[2 * q + 1]);
+    s_hdr[q] = cell_header(P.tab, (2 * q + Mrkv) * n_J + jc);
   }
   __syncthreads();
   double local = 0.0;
@@ -148,68 +134,22 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) uu[k] = 0.37 + 1e-9 * (double)(idx[k] & 1023);
 #endif
+    int cell[kAgents];
+    CellHdr hh[kAgents];
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
       int l = 0;
       for (int q = 0; q < n_lab; ++q) l += (s_cdf[lp[k] * n_lab + q] <= uu[k]) ? 1 : 0;  // searchsorted(cdf, u, 'right')
       ln[k] = l;
       m[k] = Rnow * ap[k] + Wnow * (s_lvl[l] * 1.0);                                    // AS:1283
+      cell[k] = (2 * l + Mrkv) * n_J + jc;                                              // employed (Urate = 0)
+      hh[k] = s_hdr[l];
     }
-#ifdef AIY_DIAG_NO_LOOKUP
+    double c[kAgents];
+    tab_policy<kAgents>(P.tab, cell, hh, m, alpha, n_M > 1, c);                          // AS:1326-1408
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
-      const double an = m[k] * 0.9;  // diagnostic build only: no policy lookup
-      if (ok[k]) { r.a[idx[k]] = an; r.lab[idx[k]] = (uint8_t)ln[k]; local += an; }
-    }
-    continue;
-#endif
-    // hop 1: index windows of both M rows of every agent (independent loads)
-    int lo[2 * kAgents], hi[2 * kAgents];
-    const double2* pr[2 * kAgents];
-#pragma unroll
-    for (int k = 0; k < kAgents; ++k) {
-      const int s = 4 * ln[k] + 2 * Mrkv + 1;                                            // employed (Urate = 0)
-      const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
-      pr[2 * k] = P.pol_pairs + r0 * n1;
-      pr[2 * k + 1] = P.pol_pairs + r1 * n1;
-      panel_window(P.pol_index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
-                                 lo[2 * k], hi[2 * k]);
-      panel_window(P.pol_index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
-                                 m[k], lo[2 * k + 1], hi[2 * k + 1]);
-    }
-    // lock-step bracket searches of all 2 kAgents rows (windows hold ~1 node)
-    bool more = false;
-#pragma unroll
-    for (int q = 0; q < 2 * kAgents; ++q) more = more || (lo[q] < hi[q]);
-    while (more) {
-      more = false;
-      double v[2 * kAgents];
-      int mid[2 * kAgents];
-#pragma unroll
-      for (int q = 0; q < 2 * kAgents; ++q) {
-        mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
-        v[q] = lo[q] < hi[q] ? pr[q][mid[q]].x : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 2 * kAgents; ++q) {
-        if (lo[q] < hi[q]) {
-          if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
-          more = more || (lo[q] < hi[q]);
-        }
-      }
-    }
-    // bracket pairs (independent loads), HARK lerp, LinearInterpOnInterp1D blend
-#pragma unroll
-    for (int k = 0; k < kAgents; ++k) {
-      const int i0 = lo[2 * k] < 1 ? 1 : lo[2 * k];
-      const int i1 = lo[2 * k + 1] < 1 ? 1 : lo[2 * k + 1];
-      const double f0 = lerp_pair(pr[2 * k], i0, m[k], kBorrowNodeOf(pr[2 * k]));
-      double c = f0;
-      if (n_M > 1) {
-        const double f1 = lerp_pair(pr[2 * k + 1], i1, m[k], kBorrowNodeOf(pr[2 * k + 1]));
-        c = (1 - alpha) * f0 + alpha * f1;                                             // LinearInterpOnInterp1D
-      }
-      const double an = m[k] - c;                                                       // AS:1415
+      const double an = m[k] - c[k];                                                    // AS:1415
       if (ok[k]) {
         r.a[idx[k]] = an;
         r.lab[idx[k]] = (uint8_t)ln[k];
@@ -323,13 +263,9 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
                                    aiy_stream stream) {
   if (!h) return AIY_ERR_ARG;
   if (!model || !mkt || !sow) return fail(h, AIY_ERR_ARG, "null model/market/sow");
-  if (model->S < 1 || model->n_M < 1 || model->n_a < 2 || model->n_lab < 1 || model->n_lab > 255)
-    return fail(h, AIY_ERR_ARG, "bad model sizes");
-  if (model->S < 4 * model->n_lab) return fail(h, AIY_ERR_ARG, "S must be 4 * n_lab (KS form)");
-  if (model->n_lab > kLdsLab) return fail(h, AIY_ERR_UNSUPPORTED, "n_lab=%d > %d", model->n_lab, kLdsLab);
-  if (!model->lab_level || !model->lab_cdf || !model->mrkv_hist || !model->pol_pairs || !model->pol_index)
-    return fail(h, AIY_ERR_ARG, "null model array (pol_pairs/pol_index come from aiy_panel_prepare)");
-  if (model->n_M > 1 && !model->M_grid) return fail(h, AIY_ERR_ARG, "null M_grid");
+  PanelDev P;
+  int32_t rc = panel_dev(h, model, P);
+  if (rc) return rc;
   if (n_local < 0 || n_total < 1 || agent_offset < 0) return fail(h, AIY_ERR_ARG, "bad agent counts");
   if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
   if (u && u_ld < n_local) return fail(h, AIY_ERR_ARG, "u_ld < n_local");
@@ -338,15 +274,10 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   if (!h->comm && n_local != n_total) return fail(h, AIY_ERR_ARG, "n_local != n_total without a communicator");
   if (n_periods == 0) return AIY_OK;
   AIY_HIP(h, hipSetDevice(h->device));
-  int32_t rc = ensure_panel_scratch(h);
+  rc = ensure_panel_scratch(h);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
   const int nb = sim_blocks(n_local);
-  PanelDev P;
-  P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
-  P.M_grid = model->M_grid;
-  P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
-  P.pol_index = model->pol_index; P.pol_pairs = reinterpret_cast<const double2*>(model->pol_pairs);
   PanelRun r;
   r.n = n_local; r.offset = agent_offset; r.n_total = n_total; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld;
   r.u_t0 = t0; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
@@ -404,15 +335,13 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   if (!h) return AIY_ERR_ARG;
   if (!model || !mkt || !sow || !a || !lab || !ms_out || n_local < 1 || n_launch < 1)
     return fail(h, AIY_ERR_ARG, "bad arguments");
+  PanelDev P;
+  int32_t rc = panel_dev(h, model, P);
+  if (rc) return rc;
   AIY_HIP(h, hipSetDevice(h->device));
-  int32_t rc = ensure_panel_scratch(h);
+  rc = ensure_panel_scratch(h);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
-  PanelDev P;
-  P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
-  P.M_grid = model->M_grid;
-  P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf; P.mrkv_hist = model->mrkv_hist;
-  P.pol_index = model->pol_index; P.pol_pairs = reinterpret_cast<const double2*>(model->pol_pairs);
   PanelRun r;
   r.n = n_local; r.offset = 0; r.n_total = n_local; r.a = a; r.lab = lab; r.u = nullptr; r.u_ld = 0; r.u_t0 = 0;
   r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;

@@ -10,8 +10,8 @@
 //   -> a = m - c (AS:1415) -> workgroup reduction of a (fixed order) -> calc_R_and_W
 //   (AS:1867-1894) by lane 0 -> barrier,
 // with no grid-wide synchronisation (calibrations are independent) and no memory
-// traffic for the agents themselves.  Policy lookups use the same interleaved pairs
-// and PanelIdx search index as the large-panel kernel (aiy_panel_prepare).
+// traffic for the agents themselves.  Policy lookups use the same merged tables as the
+// large-panel kernels (aiy_panel_build, panel_common.h).
 #include "common.h"
 #include "internal.h"
 #include "panel_common.h"
@@ -23,8 +23,8 @@ namespace aiy {
 
 struct BatchDev {
   int n_cal, S, n_M, n_a, n_lab, act_T;
-  const double2* pol_pairs;  // [n_cal][S][n_M][n1]
-  const int* pol_index;      // [n_cal][S * n_M][PanelIdx::kRow]
+  const char* tables;        // [n_cal][g.bytes] merged policy tables
+  PanelTabGeom g;
   const double* M_grid;      // [n_cal][n_M]
   const double* lab_level;   // [n_cal][n_lab]
   const double* lab_cdf;     // [n_cal][n_lab][n_lab]
@@ -59,9 +59,9 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
   const int nthr = blockDim.x;
   const int n = (int)r.n;
   uint8_t* s_lab = reinterpret_cast<uint8_t*>(s_a + n);
-  const int n_M = B.n_M, n_a = B.n_a, n1 = n_a + 1, n_lab = B.n_lab;
-  const double2* pairs = B.pol_pairs + (size_t)cal * B.S * n_M * n1;
-  const int* index = B.pol_index + (size_t)cal * B.S * n_M * PanelIdx::kRow;
+  const int n_M = B.n_M, n_lab = B.n_lab;
+  const PanelTab T = panel_tab(B.tables + (size_t)cal * B.g.bytes, B.g);
+  const int n_J = B.g.n_J;
   const double* Mg = B.M_grid + (size_t)cal * n_M;
   const int* hist = B.mrkv_hist + (size_t)cal * B.act_T;
   const aiy_market mk = r.mk[cal];
@@ -72,8 +72,7 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
 
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
-  __shared__ int s_base[2 * kLdsLab];
-  __shared__ int s_last[2 * kLdsLab];
+  __shared__ CellHdr s_hdr[kLdsLab];
   __shared__ double s_red[kBlkMaxThreads / kWave];
   __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = B.lab_cdf[(size_t)cal * n_lab * n_lab + q];
@@ -96,22 +95,10 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
     const int t = r.t0 + p;
     const double Mnow = s_price[0], Rnow = s_price[1], Wnow = s_price[2];
     const int Mrkv = (int)s_price[3];
-    int j = 1;
-    double alpha = 0.0;
-    if (n_M > 1) {
-      j = lower_bound(Mg, 0, n_M, Mnow);
-      j = j > n_M - 1 ? n_M - 1 : j;
-      j = j < 1 ? 1 : j;
-      alpha = (Mnow - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
-    }
-    const int jlo = n_M > 1 ? j - 1 : 0, jhi = n_M > 1 ? j : 0;
-    for (int q = tid; q < n_lab; q += nthr) {
-      const int s = 4 * q + 2 * Mrkv + 1;
-      const int* h0 = index + ((size_t)s * n_M + jlo) * PanelIdx::kRow;
-      const int* h1 = index + ((size_t)s * n_M + jhi) * PanelIdx::kRow;
-      brk_header(h0, s_base[2 * q], s_last[2 * q]);
-      brk_header(h1, s_base[2 * q + 1], s_last[2 * q + 1]);
-    }
+    int jc;
+    double alpha;
+    m_bracket(Mg, n_M, Mnow, jc, alpha);
+    for (int q = tid; q < n_lab; q += nthr) s_hdr[q] = cell_header(T, (2 * q + Mrkv) * n_J + jc);
     __syncthreads();
     const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
     const double* u = r.u ? r.u + ((size_t)cal * r.n_periods + p) * n : nullptr;
@@ -141,52 +128,20 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
           m[k] = Rnow * s_a[i] + Wnow * (s_lvl[l] * 1.0);                                // AS:1283
         }
       }
-      int lo[2 * A], hi[2 * A];
-      const double2* pr[2 * A];
+      int cell[A];
+      CellHdr hh[A];
 #pragma unroll
       for (int k = 0; k < A; ++k) {
-        const int s = 4 * ln[k] + 2 * Mrkv + 1;                                          // employed (Urate = 0)
-        const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
-        pr[2 * k] = pairs + r0 * n1;
-        pr[2 * k + 1] = pairs + r1 * n1;
-        panel_window(index + r0 * PanelIdx::kRow, s_base[2 * ln[k]], s_last[2 * ln[k]], n_a, m[k],
-                                   lo[2 * k], hi[2 * k]);
-        panel_window(index + r1 * PanelIdx::kRow, s_base[2 * ln[k] + 1], s_last[2 * ln[k] + 1], n_a,
-                                   m[k], lo[2 * k + 1], hi[2 * k + 1]);
+        cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                        // employed (Urate = 0)
+        hh[k] = s_hdr[ln[k]];
       }
-      bool more = false;
-#pragma unroll
-      for (int q = 0; q < 2 * A; ++q) more = more || (lo[q] < hi[q]);
-      while (more) {
-        more = false;
-        double v[2 * A];
-        int mid[2 * A];
-#pragma unroll
-        for (int q = 0; q < 2 * A; ++q) {
-          mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
-          v[q] = lo[q] < hi[q] ? pr[q][mid[q]].x : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < 2 * A; ++q) {
-          if (lo[q] < hi[q]) {
-            if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
-            more = more || (lo[q] < hi[q]);
-          }
-        }
-      }
+      double c[A];
+      tab_policy<A>(T, cell, hh, m, alpha, n_M > 1, c);                                  // AS:1326-1408
 #pragma unroll
       for (int k = 0; k < A; ++k) {
-        const int b0 = lo[2 * k] < 1 ? 1 : lo[2 * k];
-        const int b1 = lo[2 * k + 1] < 1 ? 1 : lo[2 * k + 1];
-        const double f0 = lerp_pair(pr[2 * k], b0, m[k], kBorrowNodeOf(pr[2 * k]));
-        double c = f0;
-        if (n_M > 1) {
-          const double f1 = lerp_pair(pr[2 * k + 1], b1, m[k], kBorrowNodeOf(pr[2 * k + 1]));
-          c = (1 - alpha) * f0 + alpha * f1;                                             // LinearInterpOnInterp1D
-        }
         const int i = i0 + k;
         if (i < n) {
-          const double an = m[k] - c;                                                    // AS:1415
+          const double an = m[k] - c[k];                                                 // AS:1415
           s_a[i] = an;
           s_lab[i] = (uint8_t)ln[k];
           local += an;
@@ -243,8 +198,9 @@ extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* m
   const aiy_panel_batch& M = *model;
   if (M.n_cal < 1 || M.S < 1 || M.n_M < 1 || M.n_a < 2 || M.n_lab < 1 || M.n_lab > kLdsLab || M.S < 4 * M.n_lab)
     return fail(h, AIY_ERR_ARG, "bad batch model sizes");
-  if (!M.pol_pairs || !M.pol_index || !M.lab_level || !M.lab_cdf || !M.mrkv_hist || (M.n_M > 1 && !M.M_grid))
-    return fail(h, AIY_ERR_ARG, "null batch model array");
+  if (M.S != 4 * M.n_lab || 2LL * M.n_a >= BrkIdx::kMaxNodes) return fail(h, AIY_ERR_ARG, "bad batch model sizes");
+  if (!M.tables || !M.lab_level || !M.lab_cdf || !M.mrkv_hist || (M.n_M > 1 && !M.M_grid))
+    return fail(h, AIY_ERR_ARG, "null batch model array (tables come from aiy_panel_build)");
   if (n_agents < 1 || n_agents > kBlkMaxAgents) return fail(h, AIY_ERR_UNSUPPORTED, "n_agents out of range");
   if (!a || !lab) return fail(h, AIY_ERR_ARG, "null agent arrays");
   if (t0 < 0 || n_periods < 0 || (int64_t)t0 + n_periods > act_T || act_T > (1 << 20))
@@ -269,7 +225,7 @@ extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* m
   AIY_HIP(h, hipMemcpyAsync(h->d_blk, h->h_blk, need, hipMemcpyHostToDevice, st));
   BatchDev B;
   B.n_cal = M.n_cal; B.S = M.S; B.n_M = M.n_M; B.n_a = M.n_a; B.n_lab = M.n_lab; B.act_T = act_T;
-  B.pol_pairs = reinterpret_cast<const double2*>(M.pol_pairs); B.pol_index = M.pol_index; B.M_grid = M.M_grid;
+  B.tables = static_cast<const char*>(M.tables); B.g = panel_tab_geom(M.n_lab, M.n_M, M.n_a); B.M_grid = M.M_grid;
   B.lab_level = M.lab_level; B.lab_cdf = M.lab_cdf; B.mrkv_hist = M.mrkv_hist;
   BlockRun r;
   r.n = n_agents; r.a = a; r.lab = lab; r.u = u;

@@ -1,10 +1,177 @@
-// Device helpers shared by the panel kernels (panel.hip, panel_block.hip).
+// Device helpers shared by the panel kernels (panel.hip, panel_block.hip,
+// panel_resident.hip) and the merged policy tables they read (panel_tab.hip).
 #pragma once
 
 #include "common.h"
 #include "internal.h"
 
 namespace aiy {
+
+// ---------------------------------------------------------------------------------
+// Merged policy tables ("cells", built once per history by aiy_panel_build).
+//
+// get_controls (AS:1326-1408) evaluates, for an agent of labour state l in aggregate
+// state g, HARK's LinearInterpOnInterp1D of the employed sub-state s = 4 l + 2 g + 1:
+//   c = (1 - alpha) f_{j-1}(m) + alpha f_j(m),
+// two LinearInterp rows at the M nodes bracketing the period's Mnow.  Cell (l, g, j)
+// merges the two rows' searched nodes x0[0..n), x1[0..n) (n = n_a: HARK searches
+// x[:-1]) into one sorted list z[0..Z), Z = 2 n.  For q in (z[k-1], z[k]] both rows'
+// lower_bounds are constant, so record k (k = 0..Z) holds both rows' brackets
+//   {x0[i0-1], x0[i0]}, {c0[i0-1], c0[i0]}, {x1[i1-1], x1[i1]}, {c1[i1-1], c1[i1]}
+// with i = max(lower_bound, 1).  A panel lookup is then ONE bracket-index load (BrkIdx
+// encoding, common.h, over z) plus ONE 64-byte record -- instead of two index loads,
+// two bracket searches and four pair loads -- with the reference's arithmetic unchanged.
+// n_M == 1 (no aggregate dimension): row 1 = row 0.
+//
+// Per-calibration layout (bytes; sections 256-aligned):
+//   rec [cells][Z + 1][4] double2 | z [cells][Z] double | idx [cells][buckets + 2] u64
+// cells = 2 n_lab n_J, n_J = max(n_M - 1, 1), cell(l, g, j) = (2 l + g) n_J + (j - 1).
+// The index starts at z[2]: z[0] = z[1] is both rows' (1e-7, 1e-7) borrowing node
+// (AS:1503-1504), far below the first real node.
+// ---------------------------------------------------------------------------------
+struct PanelTabGeom {
+  int n, Z, n_J, n_cells;
+  int shift, buckets;       // index over z: 2^(52 - shift) buckets per octave, kTabOctaves octaves
+  long long rec_stride;     // double2 per cell
+  long long z_stride;       // doubles per cell
+  long long idx_stride;     // u64 per cell
+  long long rec_off, z_off, idx_off, bytes;
+};
+
+constexpr int kTabOctaves = 12;
+constexpr int kTabFirst = 2;   // first indexed node of z
+
+__host__ __device__ inline long long tab_align(long long b) { return (b + 255) / 256 * 256; }
+
+__host__ __device__ inline PanelTabGeom panel_tab_geom(int n_lab, int n_M, int n_a) {
+  PanelTabGeom g;
+  g.n = n_a;
+  g.Z = 2 * n_a;
+  g.n_J = n_M > 1 ? n_M - 1 : 1;
+  g.n_cells = 2 * n_lab * g.n_J;
+  int lg = 4;                                  // ~n_a buckets per octave (~Z / 2), 16 .. 8192
+  while (lg < 13 && (1 << lg) < n_a) ++lg;
+  g.shift = 52 - lg;
+  g.buckets = kTabOctaves << lg;
+  g.rec_stride = 4LL * (g.Z + 1);
+  g.z_stride = g.Z;
+  g.idx_stride = (long long)g.buckets + 2;
+  g.rec_off = 0;
+  g.z_off = tab_align((long long)g.n_cells * g.rec_stride * 16);
+  g.idx_off = tab_align(g.z_off + (long long)g.n_cells * g.z_stride * 8);
+  g.bytes = tab_align(g.idx_off + (long long)g.n_cells * g.idx_stride * 8);
+  return g;
+}
+
+struct PanelTab {
+  const double2* rec;
+  const double* z;
+  const unsigned long long* idx;
+  PanelTabGeom g;
+};
+__host__ __device__ inline PanelTab panel_tab(const void* base, const PanelTabGeom& g) {
+  const char* b = static_cast<const char*>(base);
+  PanelTab t;
+  t.rec = reinterpret_cast<const double2*>(b + g.rec_off);
+  t.z = reinterpret_cast<const double*>(b + g.z_off);
+  t.idx = reinterpret_cast<const unsigned long long*>(b + g.idx_off);
+  t.g = g;
+  return t;
+}
+
+// Per-cell header, staged in LDS: index base and last bucket, both rows' first node
+// (the NaN guard of HARK's LinearInterp below the grid).
+struct CellHdr {
+  int base, last;
+  double first0, first1;
+};
+__device__ __forceinline__ CellHdr cell_header(const PanelTab& T, int cell) {
+  const unsigned long long* E = T.idx + (size_t)cell * T.g.idx_stride;
+  const double2* r = T.rec + (size_t)cell * T.g.rec_stride;   // record 0 brackets nodes (0, 1) of both rows
+  CellHdr h;
+  h.last = (int)(long long)E[T.g.buckets];
+  h.base = (int)(long long)E[T.g.buckets + 1];
+  h.first0 = r[0].x;
+  h.first1 = r[2].x;
+  return h;
+}
+
+// c = cFunc(m, Mnow) for the NA agents of one lane (cells and headers given), in lock
+// step so the index loads, the rare searches and the record loads of all NA agents
+// overlap.  blend = false: one row (n_M == 1).
+template <int NA>
+__device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[NA], const CellHdr (&h)[NA],
+                                           const double (&m)[NA], double alpha, bool blend, double (&c)[NA]) {
+  int lo[NA], hi[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k)
+    brk_window(T.idx + (size_t)cell[k] * T.g.idx_stride, T.g.shift, T.g.buckets, h[k].base, h[k].last, T.g.Z, m[k],
+               lo[k], hi[k]);
+  bool more = false;
+#pragma unroll
+  for (int k = 0; k < NA; ++k) more = more || (lo[k] < hi[k]);
+  while (more) {   // buckets holding >= 2 merged nodes: binary search over z
+    more = false;
+    double v[NA];
+    int mid[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      mid[k] = lo[k] + ((hi[k] - lo[k]) >> 1);
+      v[k] = lo[k] < hi[k] ? T.z[(size_t)cell[k] * T.g.z_stride + mid[k]] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      if (lo[k] < hi[k]) {
+        if (v[k] < m[k]) lo[k] = mid[k] + 1; else hi[k] = mid[k];
+        more = more || (lo[k] < hi[k]);
+      }
+    }
+  }
+  double2 p0[NA], p1[NA], p2[NA], p3[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    const double2* r = T.rec + (size_t)cell[k] * T.g.rec_stride + 4 * (size_t)lo[k];
+    p0[k] = r[0];
+    p1[k] = r[1];
+    if (blend) {
+      p2[k] = r[2];
+      p3[k] = r[3];
+    } else {
+      p2[k] = p0[k];
+      p3[k] = p1[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    // HARK LinearInterp (AS:1512): alpha = (q - x_lo) / (x_hi - x_lo),
+    // y = (1 - alpha) y_lo + alpha y_hi, NaN below the row's first node
+    const double a0 = (m[k] - p0[k].x) / (p0[k].y - p0[k].x);
+    const double v0 = (1.0 - a0) * p1[k].x + a0 * p1[k].y;
+    const double f0 = (m[k] < h[k].first0) ? __builtin_nan("") : v0;
+    if (blend) {
+      const double a1 = (m[k] - p2[k].x) / (p2[k].y - p2[k].x);
+      const double v1 = (1.0 - a1) * p3[k].x + a1 * p3[k].y;
+      const double f1 = (m[k] < h[k].first1) ? __builtin_nan("") : v1;
+      c[k] = (1 - alpha) * f0 + alpha * f1;                                     // LinearInterpOnInterp1D
+    } else {
+      c[k] = f0;
+    }
+  }
+}
+
+// The period's M bracket (LinearInterpOnInterp1D: clip(searchsorted(Mgrid, M), 1,
+// n_M - 1)) as the cell's j - 1 and the blend weight.
+__device__ __forceinline__ void m_bracket(const double* __restrict__ Mg, int n_M, double Mnow, int& jc, double& alpha) {
+  jc = 0;
+  alpha = 0.0;
+  if (n_M > 1) {
+    int j = lower_bound(Mg, 0, n_M, Mnow);
+    j = j > n_M - 1 ? n_M - 1 : j;
+    j = j < 1 ? 1 : j;
+    alpha = (Mnow - Mg[j - 1]) / (Mg[j] - Mg[j - 1]);
+    jc = j - 1;
+  }
+}
 
 // One calibration's panel model on device (aiy_panel_model).
 struct PanelDev {
@@ -13,8 +180,7 @@ struct PanelDev {
   const double* lab_level;
   const double* lab_cdf;
   const int* mrkv_hist;
-  const int* pol_index;     // BrkIdx rows (aiy_panel_prepare), int32 words
-  const double2* pol_pairs; // (m, c) interleaved rows (aiy_panel_prepare)
+  PanelTab tab;
 };
 
 // calc_R_and_W (AS:1839-1894) prices from aggregate capital K (= mean of a).
@@ -41,25 +207,12 @@ __device__ __forceinline__ Prices calc_prices(const aiy_market& mk, int Mrkv, do
   return p;
 }
 
-// Bracket-index window of one policy row with its header (base, last bucket) already in
-// registers (brk_window, common.h).
-__device__ __forceinline__ void panel_window(const int* __restrict__ row, int base, int last, int n, double q, int& lo,
-                                             int& hi) {
-  brk_window(row, base, last, n, q, lo, hi);
-}
-
-__device__ __forceinline__ double lerp_pair(const double2* __restrict__ p, int i, double q, double x0) {
-  const double2 lo = p[i - 1], hi = p[i];
-  const double alpha = (q - lo.x) / (hi.x - lo.x);
-  const double v = (1.0 - alpha) * lo.y + alpha * hi.y;
-  return (q < x0) ? __builtin_nan("") : v;
-}
-
 constexpr int kLdsLab = 16;   // labour states (the KS form has S = 4 n_lab <= 64)
 constexpr int kPairs = 2;     // agent pairs per lane per pass
 constexpr int kAgents = 2 * kPairs;
 
-__device__ __forceinline__ double kBorrowNodeOf(const double2* p) { return p[0].x; }
+// Host: check the model of one calibration and fill its device view.
+int32_t panel_dev(aiy_handle* h, const aiy_panel_model* model, PanelDev& P);
 
 // Persistent panel (panel_resident.hip), used by aiy_sim_periods on a single rank.
 int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, long long n, double* a, uint8_t* lab,

@@ -42,13 +42,6 @@ constexpr unsigned long long kResTimeoutTicks = 400000000ull;  // 4 s of the 100
 constexpr size_t kResGranBytes = sizeof(unsigned long long) * 2 * 2 * kResMaxBlocks;
 constexpr size_t kResSyncBytes = kResGranBytes + 16;          // + timeout word, padded to 16 B
 
-// Row header of one policy row for the period loop: bracket-index base and last bucket, and
-// the row's first node x0 (the NaN guard of HARK's LinearInterp below the grid).
-struct RowHdr {
-  int base, last;
-  double x0;
-};
-
 struct ResRun {
   long long n, offset;       // local agents; global index of local agent 0 (Philox)
   long long chunk;           // agents per workgroup (even)
@@ -122,9 +115,9 @@ __device__ __forceinline__ void bitonic_sort(double* A, unsigned short* perm, in
   }
 }
 
-// Dynamic LDS: [row headers (16-aligned)] [a: chunk doubles] [lab: chunk bytes]
-__host__ __device__ inline size_t res_hdr_bytes(int n_lab, int n_M) {
-  return ((size_t)n_lab * 2 * n_M * sizeof(RowHdr) + 15) / 16 * 16;
+// Dynamic LDS: [cell headers (16-aligned)] [a: chunk doubles] [lab: chunk bytes]
+__host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
+  return ((size_t)n_cells * sizeof(CellHdr) + 15) / 16 * 16;
 }
 
 template <bool IN_LDS, int kResA, bool SORT>
@@ -139,20 +132,20 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
   const int tid = threadIdx.x;
   const int nthr = blockDim.x;
   const int nb = gridDim.x;
-  const int n_M = P.n_M, n_a = P.n_a, n1 = n_a + 1, n_lab = P.n_lab;
+  const int n_M = P.n_M, n_lab = P.n_lab, n_J = P.tab.g.n_J, n_cells = P.tab.g.n_cells;
   const long long start = (long long)blockIdx.x * r.chunk;
   const int cnt = (int)std::max(0LL, std::min(r.chunk, r.n - start));
-  RowHdr* hdr = reinterpret_cast<RowHdr*>(s_dyn);   // [(2 q + Mrkv) n_M + j]
+  CellHdr* hdr = reinterpret_cast<CellHdr*>(s_dyn);   // [cell]
   double* A;
   uint8_t* L;
   unsigned short* perm = nullptr;    // SORT: agent (slice index) at sorted position k
   const int P2 = SORT ? (int)r.sort_len : 0;
   if constexpr (SORT) {
-    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_lab, n_M));
+    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_cells));
     perm = reinterpret_cast<unsigned short*>(A + P2);
     L = reinterpret_cast<uint8_t*>(perm + P2);
   } else if constexpr (IN_LDS) {
-    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_lab, n_M));
+    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_cells));
     L = reinterpret_cast<uint8_t*>(A + r.chunk);
   } else {
     A = r.a + start;
@@ -162,13 +155,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
 
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = P.lab_cdf[q];
   for (int q = tid; q < n_lab; q += nthr) s_lvl[q] = P.lab_level[q];
-  for (int q = tid; q < n_lab * 2 * n_M; q += nthr) {
-    const int j = q % n_M, qe = q / n_M;               // qe = 2 l + Mrkv
-    const int s = 4 * (qe >> 1) + 2 * (qe & 1) + 1;    // employed sub-state of labour l, aggregate Mrkv
-    const size_t row = (size_t)s * n_M + j;
-    brk_header(P.pol_index + row * PanelIdx::kRow, hdr[q].base, hdr[q].last);
-    hdr[q].x0 = P.pol_pairs[row * n1].x;
-  }
+  for (int q = tid; q < n_cells; q += nthr) hdr[q] = cell_header(P.tab, q);
   if constexpr (SORT) {
     for (int i = tid; i < P2; i += nthr) {
       A[i] = i < cnt ? r.a[start + i] : __builtin_inf();
@@ -207,15 +194,9 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     }
     const double Mnow = s_price[0], Rnow = s_price[1], Wnow = s_price[2];
     const int Mrkv = (int)s_price[3];
-    int j = 1;
-    double alpha = 0.0;
-    if (n_M > 1) {
-      j = lower_bound(P.M_grid, 0, n_M, Mnow);
-      j = j > n_M - 1 ? n_M - 1 : j;
-      j = j < 1 ? 1 : j;
-      alpha = (Mnow - P.M_grid[j - 1]) / (P.M_grid[j] - P.M_grid[j - 1]);
-    }
-    const int jlo = n_M > 1 ? j - 1 : 0, jhi = n_M > 1 ? j : 0;
+    int jc;
+    double alpha;
+    m_bracket(P.M_grid, n_M, Mnow, jc, alpha);
     __syncthreads();   // this period's labour draws complete
     AIY_PH(0);
 
@@ -239,56 +220,26 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
         if (g0 + k < cnt) { A[pos[k]] = 0.9 * m[k]; local += 0.9 * m[k]; }   // diagnostic build only
       continue;
 #endif
-      int lo[2 * kResA], hi[2 * kResA];
-      double x0[2 * kResA];
-      const double2* pr[2 * kResA];
+      int cell[kResA];
+      CellHdr hh[kResA];
 #pragma unroll
       for (int k = 0; k < kResA; ++k) {
-        const int s = 4 * ln[k] + 2 * Mrkv + 1;                                             // employed (Urate = 0)
-        const size_t r0 = (size_t)s * n_M + jlo, r1 = (size_t)s * n_M + jhi;
-        const RowHdr h0 = hdr[(2 * ln[k] + Mrkv) * n_M + jlo];
-        const RowHdr h1 = hdr[(2 * ln[k] + Mrkv) * n_M + jhi];
-        pr[2 * k] = P.pol_pairs + r0 * n1;
-        pr[2 * k + 1] = P.pol_pairs + r1 * n1;
-        x0[2 * k] = h0.x0;
-        x0[2 * k + 1] = h1.x0;
-        panel_window(P.pol_index + r0 * PanelIdx::kRow, h0.base, h0.last, n_a, m[k], lo[2 * k],
-                                   hi[2 * k]);
-        panel_window(P.pol_index + r1 * PanelIdx::kRow, h1.base, h1.last, n_a, m[k], lo[2 * k + 1],
-                                   hi[2 * k + 1]);
+        cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                           // employed (Urate = 0)
+        hh[k] = hdr[cell[k]];
       }
-      bool more = false;
+      double c[kResA];
+#ifdef AIY_DIAG_SAME_Q
+      double mq[kResA];   // diagnostic build only: every agent looks up the same query
 #pragma unroll
-      for (int q = 0; q < 2 * kResA; ++q) more = more || (lo[q] < hi[q]);
-      while (more) {
-        more = false;
-        double v[2 * kResA];
-        int mid[2 * kResA];
-#pragma unroll
-        for (int q = 0; q < 2 * kResA; ++q) {
-          mid[q] = lo[q] + ((hi[q] - lo[q]) >> 1);
-          v[q] = lo[q] < hi[q] ? pr[q][mid[q]].x : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < 2 * kResA; ++q) {
-          if (lo[q] < hi[q]) {
-            if (v[q] < m[q >> 1]) lo[q] = mid[q] + 1; else hi[q] = mid[q];
-            more = more || (lo[q] < hi[q]);
-          }
-        }
-      }
+      for (int k = 0; k < kResA; ++k) mq[k] = 2.0 + 1e-9 * k;
+      tab_policy<kResA>(P.tab, cell, hh, mq, alpha, n_M > 1, c);
+#else
+      tab_policy<kResA>(P.tab, cell, hh, m, alpha, n_M > 1, c);                             // AS:1326-1408
+#endif
 #pragma unroll
       for (int k = 0; k < kResA; ++k) {
-        const int b0 = lo[2 * k] < 1 ? 1 : lo[2 * k];
-        const int b1 = lo[2 * k + 1] < 1 ? 1 : lo[2 * k + 1];
-        const double f0 = lerp_pair(pr[2 * k], b0, m[k], x0[2 * k]);
-        double c = f0;
-        if (n_M > 1) {
-          const double f1 = lerp_pair(pr[2 * k + 1], b1, m[k], x0[2 * k + 1]);
-          c = (1 - alpha) * f0 + alpha * f1;                                                // LinearInterpOnInterp1D
-        }
         if (g0 + k < cnt) {
-          const double an = m[k] - c;                                                       // AS:1415
+          const double an = m[k] - c[k];                                                    // AS:1415
           A[pos[k]] = an;
           local += an;
         }
@@ -402,7 +353,7 @@ struct ResGeometry {
   size_t lds_sort = 0;
 };
 
-static ResGeometry res_geometry(aiy_handle* h, long long n, int n_lab, int n_M) {
+static ResGeometry res_geometry(aiy_handle* h, long long n, int n_cells) {
   ResGeometry G;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) cus = 1;
@@ -411,7 +362,7 @@ static ResGeometry res_geometry(aiy_handle* h, long long n, int n_lab, int n_M) 
   G.chunk = (n + G.nb - 1) / G.nb;
   G.chunk += G.chunk & 1;                            // even: Philox pairs never straddle workgroups
   G.nb = (int)((n + G.chunk - 1) / G.chunk);
-  const size_t hdr = res_hdr_bytes(n_lab, n_M);
+  const size_t hdr = res_hdr_bytes(n_cells);
   const size_t agents = (size_t)G.chunk * (sizeof(double) + 1);
   G.in_lds = hdr + agents <= kResLdsBudget;
   G.lds = G.in_lds ? (hdr + agents + 15) / 16 * 16 : hdr;
@@ -423,7 +374,7 @@ static ResGeometry res_geometry(aiy_handle* h, long long n, int n_lab, int n_M) 
   return G;
 }
 
-bool resident_supported(const PanelDev& P) { return res_hdr_bytes(P.n_lab, P.n_M) <= kResHdrMaxBytes; }
+bool resident_supported(const PanelDev& P) { return res_hdr_bytes(P.tab.g.n_cells) <= kResHdrMaxBytes; }
 
 static int32_t ensure_res_scratch(aiy_handle* h) {
   if (!h->d_res_sync) {
@@ -437,7 +388,7 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
                         int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
   if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
-  const ResGeometry G = res_geometry(h, n, P.n_lab, P.n_M);
+  const ResGeometry G = res_geometry(h, n, P.tab.g.n_cells);
   int32_t rc = ensure_res_scratch(h);
   if (rc) return rc;
   const void* kernels[3][2] = {

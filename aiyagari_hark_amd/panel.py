@@ -71,24 +71,15 @@ class DevicePanel:
     def bind_model(self, m_pol, c_pol, M_grid, lab_level, lab_cdf, mrkv_hist, market: dict):
         S, n_M, n1 = m_pol.shape
         n_lab = int(lab_level.numel())
-        keep = dict(m_pol=m_pol.contiguous(), c_pol=c_pol.contiguous(), M_grid=M_grid.contiguous(),
-                    lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
+        keep = dict(M_grid=M_grid.contiguous(), lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
                     mrkv_hist=mrkv_hist.to(torch.int32).contiguous())
-        # interleaved (m, c) pairs + fine log-bucket search index (built on device once per history)
+        # merged policy tables (aiy_panel_build, once per history)
         h = _lib.handle(self.device.index)
-        ipr = h.lib.aiy_panel_index_ints_per_row()
-        keep["pol_pairs"] = torch.empty((S, n_M, n1, 2), dtype=F64, device=self.device)
-        keep["pol_index"] = torch.empty((S * n_M, ipr), dtype=torch.int32, device=self.device)
-        h.check(h.lib.aiy_panel_prepare(h.h, S * n_M, n1, _lib.ptr(keep["m_pol"]), _lib.ptr(keep["c_pol"]),
-                                        _lib.ptr(keep["pol_pairs"]), _lib.ptr(keep["pol_index"]), _lib.stream_ptr()),
-                "aiy_panel_prepare")
-        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
-                                                       ("pol_pairs", "pol_index", "M_grid", "lab_level", "lab_cdf",
-                                                        "mrkv_hist")))
+        keep["tables"] = build_tables(h, m_pol[None], c_pol[None], n_lab, self.device)
+        ptrs = [_lib.ptr(keep[k]) for k in ("tables", "M_grid", "lab_level", "lab_cdf", "mrkv_hist")]
+        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *ptrs)
         mk = make_market(market)
-        pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
-                                                          ("pol_pairs", "pol_index", "M_grid", "lab_level", "lab_cdf",
-                                                           "mrkv_hist")))
+        pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *ptrs)
         self._model = (pm, mk, keep, pb)
 
     def run(self, t0: int, n_periods: int, shock_mode="philox", seed=0, ge_iter=0, u_host_source=None,
@@ -141,6 +132,21 @@ class DevicePanel:
 def make_market(market: dict) -> "_lib.Market":
     return _lib.Market(market["CapShare"], market["DeprFac"], (ctypes.c_double * 2)(*market["prod"]),
                        (ctypes.c_double * 2)(*market["agg_L"]))
+
+
+def build_tables(h, m_pol, c_pol, n_lab, device):
+    """Merged policy tables of n_cal calibrations (aiy_panel_build): m_pol/c_pol
+    [n_cal, S, n_M, n_a + 1] device tensors -> uint8 tensor [n_cal, table bytes]."""
+    n_cal, S, n_M, n1 = m_pol.shape
+    nbytes = int(h.lib.aiy_panel_table_bytes(n_lab, n_M, n1 - 1))
+    if nbytes <= 0:
+        raise _lib.AiyagariLibError(f"unsupported panel table sizes n_lab={n_lab} n_M={n_M} n_a={n1 - 1}")
+    tables = torch.empty((n_cal, nbytes), dtype=torch.uint8, device=device)
+    m_pol = m_pol.contiguous()
+    c_pol = c_pol.contiguous()
+    h.check(h.lib.aiy_panel_build(h.h, n_cal, S, n_M, n1 - 1, n_lab, _lib.ptr(m_pol), _lib.ptr(c_pol),
+                                  _lib.ptr(tables), _lib.stream_ptr()), "aiy_panel_build")
+    return tables
 
 
 def run_block(h, pb, markets_ref, n_agents, a, lab, seeds, ge_iter, t0, n_periods, act_T, sow, hist_A, hist_M,
@@ -210,18 +216,12 @@ class BatchedPanel:
             raise ValueError("calibration count mismatch")
         n_lab = int(lab_level.shape[1])
         h = _lib.handle(self.device.index)
-        ipr = h.lib.aiy_panel_index_ints_per_row()
-        keep = dict(m_pol=m_pol.contiguous(), c_pol=c_pol.contiguous(), M_grid=M_grid.contiguous(),
-                    lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
+        keep = dict(M_grid=M_grid.contiguous(), lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
                     mrkv_hist=mrkv_hist.to(torch.int32).contiguous())
-        keep["pol_pairs"] = torch.empty((n_cal, S, n_M, n1, 2), dtype=F64, device=self.device)
-        keep["pol_index"] = torch.empty((n_cal * S * n_M, ipr), dtype=torch.int32, device=self.device)
-        h.check(h.lib.aiy_panel_prepare(h.h, n_cal * S * n_M, n1, _lib.ptr(keep["m_pol"]), _lib.ptr(keep["c_pol"]),
-                                        _lib.ptr(keep["pol_pairs"]), _lib.ptr(keep["pol_index"]), _lib.stream_ptr()),
-                "aiy_panel_prepare")
+        keep["tables"] = build_tables(h, m_pol, c_pol, n_lab, self.device)
         pb = _lib.PanelBatch(n_cal, S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
-                                                              ("pol_pairs", "pol_index", "M_grid", "lab_level",
-                                                               "lab_cdf", "mrkv_hist")))
+                                                              ("tables", "M_grid", "lab_level", "lab_cdf",
+                                                               "mrkv_hist")))
         mks = (_lib.Market * n_cal)(*(make_market(m) for m in markets))
         self._model = (pb, mks, keep)
 

@@ -133,10 +133,9 @@ typedef struct {
 
 /* Household panel model for one calibration (policy fixed during a history). */
 typedef struct {
-  int32_t S, n_M, n_a, n_lab;
-  const double* pol_pairs;  /* [S][n_M][n_a+1][2] (m, c) pairs of the converged policy
-                               (AiyagariType.solution[0]), from aiy_panel_prepare          */
-  const int32_t* pol_index; /* [S][n_M][aiy_panel_index_ints_per_row()], aiy_panel_prepare */
+  int32_t S, n_M, n_a, n_lab; /* S = 4 n_lab (KS form)                                       */
+  const void* tables;       /* merged policy tables of the converged policy
+                               (AiyagariType.solution[0]), from aiy_panel_build              */
   const double* M_grid;     /* [n_M]                                                       */
   const double* lab_level;  /* [n_lab] LSStates (AS:1265)                                  */
   const double* lab_cdf;    /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
@@ -144,15 +143,20 @@ typedef struct {
                                a call simulates (t0 + n_periods <= act_T)                    */
 } aiy_panel_model;
 
-/* Prepare a policy table [n_rows = S * n_M][n1] for the panel: interleave (m, c) into
- * pairs [n_rows][n1][2] and build the bracket index of every row: 4 096 log buckets per
- * binary octave, one 64-bit entry per bucket holding the lower_bound of the bucket edge,
- * the number of nodes in the bucket and the low bits of its first node, so a panel
- * lookup is one index load plus the bracketing pair loads, with no search step when the
- * bucket holds at most one node.  n1 <= 2^21.  Asynchronous. */
-int32_t aiy_panel_index_ints_per_row(void);
-int32_t aiy_panel_prepare(aiy_handle* h, int64_t n_rows, int32_t n1, const double* m_pol,
-                          const double* c_pol, double* pairs, int32_t* index, aiy_stream stream);
+/* Panel policy tables (get_controls, AS:1326-1408).  Each period an agent of labour
+ * state l evaluates LinearInterpOnInterp1D = (1 - alpha) f_{j-1}(m) + alpha f_j(m) of
+ * its employed sub-state s = 4 l + 2 Mrkv + 1.  For every (l, Mrkv, M interval j) the
+ * two rows' nodes are merged into one sorted list; on each merged segment both rows'
+ * brackets are fixed, so one 64-byte record holds both, and a bracket index over the
+ * merged nodes (log buckets, one 64-bit entry each) finds the record with no search
+ * in the common case.  HARK's arithmetic is unchanged (results bit-identical to
+ * searching the two rows).
+ *   aiy_panel_table_bytes: bytes of ONE calibration's tables (-1: unsupported sizes)
+ *   aiy_panel_build: m_pol, c_pol [n_cal][S][n_M][n_a+1] (device) -> tables
+ *                    [n_cal][aiy_panel_table_bytes] (device).  Asynchronous. */
+int64_t aiy_panel_table_bytes(int32_t n_lab, int32_t n_M, int32_t n_a);
+int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, int32_t n_a, int32_t n_lab,
+                        const double* m_pol, const double* c_pol, void* tables, aiy_stream stream);
 
 /* Device-resident market state ("sow_state", AS:1585), 8 doubles:
  *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] sum(a) [7] period index t */
@@ -198,8 +202,7 @@ int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const a
  * All calibrations share (S, n_M, n_a, n_lab); arrays are stacked over calibrations. */
 typedef struct {
   int32_t n_cal, S, n_M, n_a, n_lab;
-  const double* pol_pairs;  /* [n_cal][S][n_M][n_a+1][2], aiy_panel_prepare */
-  const int32_t* pol_index; /* [n_cal][S][n_M][aiy_panel_index_ints_per_row()] */
+  const void* tables;       /* [n_cal][aiy_panel_table_bytes], aiy_panel_build */
   const double* M_grid;     /* [n_cal][n_M] */
   const double* lab_level;  /* [n_cal][n_lab] */
   const double* lab_cdf;    /* [n_cal][n_lab][n_lab] */

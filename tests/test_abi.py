@@ -52,8 +52,8 @@ def test_struct_layouts(lib):
     assert ctypes.sizeof(_lib.EgmDims) == 16
     assert ctypes.sizeof(_lib.EgmInputs) == 9 * 8
     assert ctypes.sizeof(_lib.Market) == 6 * 8
-    assert ctypes.sizeof(_lib.PanelModel) == 16 + 6 * 8
-    assert ctypes.sizeof(_lib.PanelBatch) == 24 + 6 * 8
+    assert ctypes.sizeof(_lib.PanelModel) == 16 + 5 * 8
+    assert ctypes.sizeof(_lib.PanelBatch) == 24 + 5 * 8
 
 
 def test_argument_validation_without_gpu(lib):
@@ -85,3 +85,15 @@ def test_missing_library_fails_loudly(tmp_path):
             _lib.load(str(tmp_path / "nope.so"))
     finally:
         _lib._lib = saved
+
+
+def test_panel_table_bytes_host_only(lib):
+    """aiy_panel_table_bytes is pure host arithmetic: sizes grow with the grid, and
+    unsupported shapes are refused with -1 before any device work."""
+    small = lib.aiy_panel_table_bytes(7, 15, 32)
+    big = lib.aiy_panel_table_bytes(7, 15, 10000)
+    assert 0 < small < big
+    assert small % 256 == 0 and big % 256 == 0
+    assert lib.aiy_panel_table_bytes(7, 15, 1) == -1
+    assert lib.aiy_panel_table_bytes(0, 15, 32) == -1
+    assert lib.aiy_panel_table_bytes(17, 15, 32) == -1

@@ -349,13 +349,14 @@ def test_search_index_equals_binary_search(gpu):
             assert H[r, b] == np.searchsorted(xr, edge), (r, b)
 
 
-def _brk_bracket(E, n, q, shift=40, n_buckets=16 * 4096):
-    """Host restatement of brk_window (csrc/common.h) on one bracket-index row E
-    (uint64): the lower_bound of q over x[0..n), or (lo, hi) when a search remains."""
+def _brk_window(E, shift, n_buckets, n, q):
+    """Host restatement of brk_window (csrc/common.h): the search window [lo, hi) of
+    lower_bound(z[0..n), q) read from one bracket index E (uint64); lo == hi: resolved."""
     last, base = int(np.int64(E[n_buckets])), int(np.int64(E[n_buckets + 1]))
     bits = int(np.float64(q).view(np.uint64))
     key = (bits >> shift) - base
     lo_of = lambda e: int(e) >> 43  # noqa: E731
+    low = (1 << 40) - 1
     if not q > 0 or key < 0:
         return 0, lo_of(E[0])
     if key >= n_buckets - 1:
@@ -363,52 +364,96 @@ def _brk_bracket(E, n, q, shift=40, n_buckets=16 * 4096):
     if key > last:
         return n, n
     e = int(E[key])
-    lo, cnt, low = lo_of(e), (e >> 40) & 7, e & ((1 << 40) - 1)
+    lo, cnt = lo_of(e), (e >> 40) & 7
     if cnt == 0:
         return lo, lo
     if cnt == 1:
-        i = lo + (1 if low < (bits & ((1 << 40) - 1)) else 0)
-        return i, i
+        t = max(shift - 40, 0)
+        xs, qs = e & low, (bits >> t) & low
+        if xs != qs:
+            i = lo + (1 if xs < qs else 0)
+            return i, i
+        return (lo, lo) if t == 0 else (lo, lo + 1)
     return (lo, lo + cnt) if cnt < 7 else (lo, lo_of(E[key + 1]))
 
 
-def test_panel_bracket_index_semantics(gpu):
-    """aiy_panel_prepare's bracket index: for queries across the whole row (nodes
-    themselves, their neighbours in ulps, random values, below / above the grid) the
-    decoded window always contains numpy's searchsorted(x[:-1], q) and is a single
-    point whenever the bucket holds at most one node."""
+def _tab_geom(n_lab, n_M, n_a):
+    """Host restatement of panel_tab_geom (csrc/panel_common.h)."""
+    up = lambda b: (b + 255) // 256 * 256  # noqa: E731
+    Z, n_J = 2 * n_a, max(n_M - 1, 1)
+    cells = 2 * n_lab * n_J
+    lg = 4
+    while lg < 13 and (1 << lg) < n_a:
+        lg += 1
+    buckets = 12 << lg
+    rec_off = 0
+    z_off = up(cells * 4 * (Z + 1) * 16)
+    idx_off = up(z_off + cells * Z * 8)
+    return dict(Z=Z, n_J=n_J, cells=cells, shift=52 - lg, buckets=buckets, z_off=z_off, idx_off=idx_off,
+                bytes=up(idx_off + cells * (buckets + 2) * 8), rec_off=rec_off)
+
+
+@pytest.mark.parametrize("name", ["egm_cfg1_afunc2", "big"])
+def test_panel_tables_semantics(gpu, name):
+    """aiy_panel_build: for every probed cell (labour l, aggregate state g, M interval j)
+    z is the stable merge of the two rows' searched nodes; for queries across the cell
+    (nodes, their ulp neighbours, random values, below / above the grid) the bracket
+    index window contains searchsorted(z, q), and record k = searchsorted(z, q) holds
+    exactly each row's HARK bracket nodes (max(searchsorted(x[:-1], q), 1) - 1, + 0)."""
     from aiyagari_hark_amd import _lib
-    fx = np.load(os.path.join(GOLD, "egm_cfg1_afunc2.npz"))
-    m = np.ascontiguousarray(fx["m"][:3, :2])          # 6 rows of 33 nodes
+    from aiyagari_hark_amd.panel import build_tables
     rng = np.random.default_rng(2)
-    big = np.sort(np.concatenate([[1e-7], np.cumsum(rng.exponential(0.004, 3000)) + 0.3]))
-    rows = [r for r in m.reshape(-1, m.shape[-1])] + [big[: m.shape[-1]]]
-    n1 = m.shape[-1]
-    X = np.stack(rows)
+    if name == "big":   # a 3000-node policy (config-2 density) built from one fixture row pair
+        S, n_M, n_a = 28, 3, 3000
+        base = np.sort(np.concatenate([[1e-7], 0.3 + np.cumsum(rng.exponential(0.004, n_a))]))
+        m = np.stack([base * (1.0 + 0.01 * k) + 0.001 * s for s in range(S) for k in range(n_M)])
+        m[:, 0] = 1e-7
+        m = m.reshape(S, n_M, n_a + 1)
+    else:
+        fx = np.load(os.path.join(GOLD, name + ".npz"))
+        m = np.ascontiguousarray(fx["m"])
+        S, n_M, n1 = m.shape
+        n_a = n1 - 1
+    c = 0.5 * m + 0.01
+    n_lab = S // 4
     h = _lib.handle(gpu.index)
-    ipr = h.lib.aiy_panel_index_ints_per_row()
-    dm = torch.as_tensor(X).to(gpu)
-    dc = torch.as_tensor(X * 0.5).to(gpu)
-    pairs = torch.empty((X.shape[0], n1, 2), dtype=torch.float64, device=gpu)
-    idx = torch.empty((X.shape[0], ipr), dtype=torch.int32, device=gpu)
-    h.check(h.lib.aiy_panel_prepare(h.h, X.shape[0], n1, _lib.ptr(dm), _lib.ptr(dc), _lib.ptr(pairs), _lib.ptr(idx),
-                                    _lib.stream_ptr()), "aiy_panel_prepare")
+    g = _tab_geom(n_lab, n_M, n_a)
+    assert h.lib.aiy_panel_table_bytes(n_lab, n_M, n_a) == g["bytes"]
+    tab = build_tables(h, torch.as_tensor(m[None]).to(gpu), torch.as_tensor(c[None]).to(gpu), n_lab, gpu)
     torch.cuda.synchronize()
-    assert np.array_equal(pairs.cpu().numpy()[..., 0], X)
-    E_all = idx.cpu().numpy().view(np.uint64)
-    resolved = 0
-    for r, x in enumerate(X):
-        E = E_all[r]
-        xs = x[:-1]
-        n = len(xs)
-        qs = [xs, np.nextafter(xs, np.inf), np.nextafter(xs, -np.inf), rng.uniform(0, 1.2 * x[-1], 400),
-              np.array([-1.0, 0.0, 1e-9, 1e-7, x[-1] * 3, 1e6])]
-        for q in np.concatenate(qs):
-            want = int(np.searchsorted(xs, q))
-            lo, hi = _brk_bracket(E, n, float(q))
-            assert lo <= want <= hi, (r, q, lo, hi, want)
-            resolved += lo == hi
-    assert resolved > 0
+    raw = tab[0].cpu().numpy()
+    Z, n_J = g["Z"], g["n_J"]
+    rec = raw[g["rec_off"]:g["z_off"]].view(np.float64)[: g["cells"] * (Z + 1) * 8].reshape(g["cells"], Z + 1, 8)
+    zz = raw[g["z_off"]:g["idx_off"]].view(np.float64)[: g["cells"] * Z].reshape(g["cells"], Z)
+    E_all = raw[g["idx_off"]:].view(np.uint64)[: g["cells"] * (g["buckets"] + 2)].reshape(g["cells"], -1)
+    resolved = total = 0
+    for cell in sorted(set([0, 1, g["cells"] - 1] + list(rng.integers(0, g["cells"], 4)))):
+        lgc, jc = divmod(cell, n_J)
+        s = 4 * (lgc // 2) + 2 * (lgc % 2) + 1
+        j0, j1 = (jc, jc + 1) if n_M > 1 else (0, 0)
+        x0, x1 = m[s, j0], m[s, j1]
+        y0, y1 = c[s, j0], c[s, j1]
+        want_z = np.sort(np.concatenate([x0[:-1], x1[:-1]]), kind="stable")
+        assert np.array_equal(zz[cell], want_z), cell
+        rand = rng.uniform(x0[1], x0[-1], 300)
+        qs = np.concatenate([rand, want_z, np.nextafter(want_z, np.inf), np.nextafter(want_z, -np.inf),
+                             [-1.0, 0.0, 1e-9, 1e-7, 3 * x0[-1], 1e6]])
+        for iq, q in enumerate(qs):
+            k = int(np.searchsorted(want_z, q))
+            lo, hi = _brk_window(E_all[cell], g["shift"], g["buckets"], Z, float(q))
+            assert lo <= k <= hi, (cell, q, lo, hi, k)
+            if iq < len(rand):
+                resolved += lo == hi
+                total += 1
+            if k > 0 and k < Z and want_z[k - 1] == want_z[k]:
+                continue   # empty segment, never selected
+            i0 = max(int(np.searchsorted(x0[:-1], q)), 1)
+            i1 = max(int(np.searchsorted(x1[:-1], q)), 1)
+            want = [x0[i0 - 1], x0[i0], y0[i0 - 1], y0[i0], x1[i1 - 1], x1[i1], y1[i1 - 1], y1[i1]]
+            assert np.array_equal(rec[cell, k], want), (cell, q, k)
+    # random queries: at config-2 density most lookups resolve from the entry alone (at
+    # N_a = 32 the two rows' nodes sit close together and often share a bucket)
+    assert resolved > (0.8 if name == "big" else 0.2) * total
 
 
 def test_stationary_capital_supply_matches_oracle(gpu):
