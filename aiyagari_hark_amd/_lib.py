@@ -10,6 +10,7 @@ linker bind libaiyagari to the same HIP runtime instance that owns the tensors w
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -27,7 +28,7 @@ AIY_MAX_STATES = 64
 AIY_SOW_DOUBLES = 8
 AIY_OPT_USE_GRAPHS = 1
 AIY_OPT_RESIDENT = 2
-AIY_OPT_RESIDENT_ORDER = 3
+AIY_OPT_RESIDENT_SHAPE = 3
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -161,6 +162,18 @@ class Handle:
 
 
 _handles: dict[int, Handle] = {}
+
+
+def close_all():
+    """Destroy every handle while the HIP runtime is still up (registered with atexit:
+    a handle freed from a module destructor after the runtime's own teardown crashes
+    the process on exit, e.g. under rocprofv3)."""
+    while _handles:
+        _, h = _handles.popitem()
+        h.close()
+
+
+atexit.register(close_all)
 
 
 def handle(device: int | None = None) -> Handle:

@@ -148,13 +148,14 @@ __device__ __forceinline__ long long idx_key(double q) {
 // starting at a base node -- with one 64-bit entry per bucket:
 //   bits 43..63  lo  = first i with key(x_i) >= bucket (= lower_bound of the edge)
 //   bits 40..42  cnt = nodes inside the bucket (saturated at 7)
-//   bits  0..39  bits [t, t + 40) of x[lo], t = max(shift - 40, 0) (cnt >= 1)
-// All doubles of one bucket share their bits above `shift`, so for a query q in bucket
-// b with cnt == 1 the stored bits decide x[lo] < q (lower_bound = lo + 1) or x[lo] >= q
-// (lo) from the entry alone -- a lookup is ONE index load with no dependent search step
-// (cnt == 0 likewise); only a tie in the stored bits (t > 0) or cnt >= 2 leaves a
-// short search.  Layout (uint64): E[0 .. buckets - 1], E[buckets] = last bucket,
-// E[buckets + 1] = base key (int64).
+//   bits  0..39  for cnt <= 3: the top w = min(40 / cnt, shift) of the `shift`
+//                within-bucket bits of each of those nodes, node j at bits [j w, j w + w)
+// All doubles of one bucket share their bits above `shift`, so comparing q's top w
+// within-bucket bits with the stored fields counts the bucket's nodes below q: the
+// lower bound comes from the entry alone -- ONE index load, no dependent search step --
+// unless a field ties with q's when w < shift (then a one-node search) or cnt >= 4.
+// Layout (uint64): E[0 .. buckets - 1], E[buckets] = last bucket, E[buckets + 1] = base
+// key (int64).
 // ---------------------------------------------------------------------------------
 struct BrkIdx {
   static constexpr unsigned long long kLow = (1ull << 40) - 1;
@@ -165,39 +166,66 @@ struct BrkIdx {
 __host__ __device__ __forceinline__ unsigned long long brk_encode(int lo, int cnt, unsigned long long low) {
   return ((unsigned long long)lo << 43) | ((unsigned long long)cnt << 40) | (low & BrkIdx::kLow);
 }
-__host__ __device__ __forceinline__ int brk_low_shift(int shift) { return shift > 40 ? shift - 40 : 0; }
+// Width of one node's field in an entry holding cnt (1..3) nodes.
+__host__ __device__ __forceinline__ int brk_field_bits(int cnt, int shift) {
+  const int w = 40 / cnt;
+  return w < shift ? w : shift;
+}
 __device__ __forceinline__ int brk_lo(unsigned long long e) { return (int)(e >> 43); }
 
-// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket index; lo == hi
-// means the bracket is already known (the common case).
-__device__ __forceinline__ void brk_window(const unsigned long long* __restrict__ E, int shift, int buckets, int base,
-                                           int last, int n, double q, int& lo, int& hi) {
+// Bracket-index lookup in two steps, so callers can issue the entry load themselves
+// (e.g. as a buffer load) and keep many lookups in flight:
+//   brk_bucket: the entry to load (>= 0) or -1 when no entry load is needed; the rare
+//               cases (below the first bucket, capped top bucket) load here directly
+//               and leave [lo, hi) set.
+//   brk_decode: [lo, hi) from the loaded entry; lo == hi means the bracket is known.
+__device__ __forceinline__ long long brk_bucket(const unsigned long long* __restrict__ E, int shift, int buckets,
+                                                int base, int last, int n, double q, int& lo, int& hi) {
   lo = 0;
   hi = n;
-  if (base == kIdxNoBase) return;
+  if (base == kIdxNoBase) return -1;
   const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
   const long long key = (long long)(bits >> shift) - (long long)base;
-  if (!(q > 0.0) || key < 0) { lo = 0; hi = brk_lo(E[0]); }
-  else if (key >= buckets - 1) {                        // capped top bucket / beyond the span
+  if (!(q > 0.0) || key < 0) { lo = 0; hi = brk_lo(E[0]); return -1; }
+  if (key >= buckets - 1) {                             // capped top bucket / beyond the span
     if (last == buckets - 1) { lo = brk_lo(E[buckets - 1]); hi = n; } else { lo = n; hi = n; }
+    return -1;
   }
-  else if (key > last) { lo = n; hi = n; }              // above every node
-  else {
-    const unsigned long long e = E[key];
-    const int l = brk_lo(e);
-    const int c = (int)((e >> 40) & 7u);
-    if (c == 0) { lo = l; hi = l; }
-    else if (c == 1) {
-      const int t = brk_low_shift(shift);
-      const unsigned long long xs = e & BrkIdx::kLow, qs = (bits >> t) & BrkIdx::kLow;
-      if (xs != qs) { lo = l + (xs < qs ? 1 : 0); hi = lo; }   // x[l] < q  <=>  lower_bound = l + 1
-      else if (t == 0) { lo = l; hi = l; }                      // q == x[l]
-      else { lo = l; hi = l + 1; }                              // tie in the stored bits: one step
+  if (key > last) { lo = n; hi = n; return -1; }        // above every node
+  return key;
+}
+__device__ __forceinline__ void brk_decode(const unsigned long long* __restrict__ E, int shift, int n, long long key,
+                                           unsigned long long e, double q, int& lo, int& hi) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
+  const int l = brk_lo(e);
+  const int c = (int)((e >> 40) & 7u);
+  if (c == 0) { lo = l; hi = l; }
+  else if (c <= 3) {
+    const int w = brk_field_bits(c, shift);
+    const unsigned long long mask = (1ull << w) - 1;
+    const unsigned long long qf = (bits >> (shift - w)) & mask;
+    int below = 0, upto = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j < c) {
+        const unsigned long long xf = (e >> (j * w)) & mask;
+        below += xf < qf ? 1 : 0;
+        upto += xf <= qf ? 1 : 0;
+      }
     }
-    else if (c < BrkIdx::kCntSat) { lo = l; hi = l + c; }
-    else { lo = l; hi = brk_lo(E[key + 1]); }
+    lo = l + below;                                       // nodes of the bucket below q
+    hi = (w == shift) ? lo : l + upto;                    // a tie in a truncated field: search it
   }
+  else if (c < BrkIdx::kCntSat) { lo = l; hi = l + c; }
+  else { lo = l; hi = brk_lo(E[key + 1]); }
   if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }  // defensive: unsorted rows
+}
+
+// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket index.
+__device__ __forceinline__ void brk_window(const unsigned long long* __restrict__ E, int shift, int buckets, int base,
+                                           int last, int n, double q, int& lo, int& hi) {
+  const long long key = brk_bucket(E, shift, buckets, base, last, n, q, lo, hi);
+  if (key >= 0) brk_decode(E, shift, n, key, E[key], q, lo, hi);
 }
 
 // Search window [lo, hi) of lower_bound(x[0..n), q) from the row index H (base given).

@@ -42,8 +42,7 @@ struct aiy_handle {
   // resident panel: tagged partial-sum granules + timeout word; option
   void* d_res_sync = nullptr;
   bool use_resident = true;
-  int res_agents = 2;                // agents per lane per lookup pass (2 or 4)
-  int res_order = 0;                 // 0 slice order, 1 sorted by wealth, 2 sorted + rotated sweeps
+  int res_shape = 0;                 // resident workgroup shape: 0 = 512 threads x 8 agents, 1 = 1024 x 4
   // block panel: per-calibration markets + seeds (device + pinned staging)
   void* d_blk = nullptr;
   void* h_blk = nullptr;

@@ -135,7 +135,6 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
     for (int k = 0; k < kAgents; ++k) uu[k] = 0.37 + 1e-9 * (double)(idx[k] & 1023);
 #endif
     int cell[kAgents];
-    CellHdr hh[kAgents];
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
       int l = 0;
@@ -143,10 +142,9 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
       ln[k] = l;
       m[k] = Rnow * ap[k] + Wnow * (s_lvl[l] * 1.0);                                    // AS:1283
       cell[k] = (2 * l + Mrkv) * n_J + jc;                                              // employed (Urate = 0)
-      hh[k] = s_hdr[l];
     }
     double c[kAgents];
-    tab_policy<kAgents>(P.tab, cell, hh, m, alpha, n_M > 1, c);                          // AS:1326-1408
+    tab_policy<kAgents>(P.tab, cell, s_hdr, ln, m, alpha, n_M > 1, c);                          // AS:1326-1408
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
       const double an = m[k] - c[k];                                                    // AS:1415
@@ -371,11 +369,10 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
     case AIY_OPT_USE_GRAPHS: h->use_graphs = value != 0; return AIY_OK;
     case AIY_OPT_RESIDENT:
       h->use_resident = value != 0;
-      if (value == 2 || value == 4) h->res_agents = (int)value;
       return AIY_OK;
-    case AIY_OPT_RESIDENT_ORDER:
-      if (value < 0 || value > 2) return fail(h, AIY_ERR_ARG, "AIY_OPT_RESIDENT_ORDER must be 0, 1 or 2");
-      h->res_order = (int)value;
+    case AIY_OPT_RESIDENT_SHAPE:
+      if (value < 0 || value > 1) return fail(h, AIY_ERR_ARG, "AIY_OPT_RESIDENT_SHAPE must be 0 or 1");
+      h->res_shape = (int)value;
       return AIY_OK;
     default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
   }

@@ -129,14 +129,12 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
         }
       }
       int cell[A];
-      CellHdr hh[A];
 #pragma unroll
       for (int k = 0; k < A; ++k) {
         cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                        // employed (Urate = 0)
-        hh[k] = s_hdr[ln[k]];
       }
       double c[A];
-      tab_policy<A>(T, cell, hh, m, alpha, n_M > 1, c);                                  // AS:1326-1408
+      tab_policy<A>(T, cell, s_hdr, ln, m, alpha, n_M > 1, c);                                  // AS:1326-1408
 #pragma unroll
       for (int k = 0; k < A; ++k) {
         const int i = i0 + k;

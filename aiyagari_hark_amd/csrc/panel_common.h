@@ -96,28 +96,64 @@ __device__ __forceinline__ CellHdr cell_header(const PanelTab& T, int cell) {
   return h;
 }
 
-// c = cFunc(m, Mnow) for the NA agents of one lane (cells and headers given), in lock
-// step so the index loads, the rare searches and the record loads of all NA agents
-// overlap.  blend = false: one row (n_M == 1).
-template <int NA>
-__device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[NA], const CellHdr (&h)[NA],
-                                           const double (&m)[NA], double alpha, bool blend, double (&c)[NA]) {
+// Raw buffer resource over a table section (32-bit byte offsets: one address VGPR per
+// lookup, the four record loads share it through immediate offsets).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tab_rsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(unsigned)bytes, 0x00020000);
+}
+__device__ __forceinline__ unsigned long long buf_u64(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ double2 buf_f64x2(__amdgpu_buffer_rsrc_t r, unsigned off, int imm) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, imm, 0));
+}
+
+#ifdef AIY_DIAG_PHASES
+__device__ unsigned diag_search_iters;   // diagnostic build only: wave search-loop trips
+#endif
+
+// c = cFunc(m, Mnow) for the NA agents of one lane, in lock step so the index loads,
+// the rare searches and the record loads of all NA agents overlap.  Agent k uses cell
+// cell[k] whose header is hdr[hidx[k]] (LDS; read where needed, not held in registers).
+// BLEND = false: one row (n_M == 1).  Every load is unconditional and BLEND is a
+// compile-time choice: a data-dependent branch between the loads makes the compiler
+// wait for each agent's record before issuing the next (measured: 8 serial round trips).
+template <int NA, bool BLEND>
+__device__ __forceinline__ void tab_policy_t(const PanelTab& T, const int (&cell)[NA], const CellHdr* hdr,
+                                             const int (&hidx)[NA], const double (&m)[NA], double alpha,
+                                             double (&c)[NA]) {
+  const PanelTabGeom& g = T.g;
+  const __amdgpu_buffer_rsrc_t ridx = tab_rsrc(T.idx, (long long)g.n_cells * g.idx_stride * 8);
+  const __amdgpu_buffer_rsrc_t rrec = tab_rsrc(T.rec, (long long)g.n_cells * g.rec_stride * 16);
   int lo[NA], hi[NA];
+  long long key[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k)
-    brk_window(T.idx + (size_t)cell[k] * T.g.idx_stride, T.g.shift, T.g.buckets, h[k].base, h[k].last, T.g.Z, m[k],
-               lo[k], hi[k]);
+    key[k] = brk_bucket(T.idx + (size_t)cell[k] * g.idx_stride, g.shift, g.buckets, hdr[hidx[k]].base,
+                        hdr[hidx[k]].last, g.Z, m[k], lo[k], hi[k]);
+  unsigned long long e[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    const unsigned eo = (unsigned)(((long long)cell[k] * g.idx_stride + (key[k] >= 0 ? key[k] : 0)) * 8);
+    e[k] = buf_u64(ridx, eo);
+  }
+#pragma unroll
+  for (int k = 0; k < NA; ++k)
+    if (key[k] >= 0) brk_decode(T.idx + (size_t)cell[k] * g.idx_stride, g.shift, g.Z, key[k], e[k], m[k], lo[k], hi[k]);
   bool more = false;
 #pragma unroll
   for (int k = 0; k < NA; ++k) more = more || (lo[k] < hi[k]);
   while (more) {   // buckets holding >= 2 merged nodes: binary search over z
     more = false;
+#ifdef AIY_DIAG_PHASES
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(&diag_search_iters, 1u);
+#endif
     double v[NA];
     int mid[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       mid[k] = lo[k] + ((hi[k] - lo[k]) >> 1);
-      v[k] = lo[k] < hi[k] ? T.z[(size_t)cell[k] * T.g.z_stride + mid[k]] : 0.0;
+      v[k] = lo[k] < hi[k] ? T.z[(size_t)cell[k] * g.z_stride + mid[k]] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
@@ -130,15 +166,12 @@ __device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[
   double2 p0[NA], p1[NA], p2[NA], p3[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k) {
-    const double2* r = T.rec + (size_t)cell[k] * T.g.rec_stride + 4 * (size_t)lo[k];
-    p0[k] = r[0];
-    p1[k] = r[1];
-    if (blend) {
-      p2[k] = r[2];
-      p3[k] = r[3];
-    } else {
-      p2[k] = p0[k];
-      p3[k] = p1[k];
+    const unsigned off = (unsigned)(((long long)cell[k] * g.rec_stride + 4LL * lo[k]) * 16);
+    p0[k] = buf_f64x2(rrec, off, 0);
+    p1[k] = buf_f64x2(rrec, off, 16);
+    if constexpr (BLEND) {
+      p2[k] = buf_f64x2(rrec, off, 32);
+      p3[k] = buf_f64x2(rrec, off, 48);
     }
   }
 #pragma unroll
@@ -147,16 +180,24 @@ __device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[
     // y = (1 - alpha) y_lo + alpha y_hi, NaN below the row's first node
     const double a0 = (m[k] - p0[k].x) / (p0[k].y - p0[k].x);
     const double v0 = (1.0 - a0) * p1[k].x + a0 * p1[k].y;
-    const double f0 = (m[k] < h[k].first0) ? __builtin_nan("") : v0;
-    if (blend) {
+    const double f0 = (m[k] < hdr[hidx[k]].first0) ? __builtin_nan("") : v0;
+    if constexpr (BLEND) {
       const double a1 = (m[k] - p2[k].x) / (p2[k].y - p2[k].x);
       const double v1 = (1.0 - a1) * p3[k].x + a1 * p3[k].y;
-      const double f1 = (m[k] < h[k].first1) ? __builtin_nan("") : v1;
+      const double f1 = (m[k] < hdr[hidx[k]].first1) ? __builtin_nan("") : v1;
       c[k] = (1 - alpha) * f0 + alpha * f1;                                     // LinearInterpOnInterp1D
     } else {
       c[k] = f0;
     }
   }
+}
+
+template <int NA>
+__device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[NA], const CellHdr* hdr,
+                                           const int (&hidx)[NA], const double (&m)[NA], double alpha, bool blend,
+                                           double (&c)[NA]) {
+  if (blend) tab_policy_t<NA, true>(T, cell, hdr, hidx, m, alpha, c);
+  else tab_policy_t<NA, false>(T, cell, hdr, hidx, m, alpha, c);
 }
 
 // The period's M bracket (LinearInterpOnInterp1D: clip(searchsorted(Mgrid, M), 1,

@@ -2,29 +2,28 @@
 // Market.make_history in ONE launch (same per-period
 // semantics as sim_period_kernel in panel.hip).
 //
-// Geometry: one 1024-thread workgroup per CU (grid = CU count, all resident; checked by
-// the cooperative launch), each owning a contiguous, even-aligned slice of the agents.
-// When the population fits (<= ~16k agents per CU, i.e. ~4M agents on MI355X) the
-// slice's assets and labour states live in LDS for the whole launch, so per period
-// the agents cost no HBM traffic at all; otherwise they stream from HBM (same code).
+// Geometry: one workgroup of TH threads per CU (grid <= CU count, all resident; checked
+// by the cooperative launch), each owning a contiguous, even-aligned slice of the
+// agents.  When the slice fits (<= ~16k agents per CU, i.e. ~4M agents on MI355X) its
+// assets and labour states live in LDS for the whole launch, so per period the agents
+// cost no HBM traffic at all; otherwise they stream from HBM (same code).
 //
 // One period, per workgroup:
-//   1. m = R a + W l, c = cFunc[4 l + 2 Mrkv + 1](m, M) (bracket-index lookup), a = m - c,
-//      partial sum of a (fixed order);
-//   2. arrive: partial stored write-through (sc1), drained, counted on one of 8 group
-//      counters, the group's last arriver counts on the top counter (monotonic counts,
-//      no resets); the global last arriver sums the partials in fixed order, runs
-//      calc_R_and_W (AS:1867-1894), stores sow/history write-through and raises the
-//      period flag (MI355X_MICROARCH.md visibility, "sc1 payload + drained flag");
-//   3. while the last arriver works, everyone draws NEXT period's labour states
-//      (Philox + inverse CDF, AS:1253-1254): they do not depend on prices, so the
-//      draw hides behind the barrier;
-//   4. lane 0 polls the flag (relaxed, s_sleep, bounded by a wall-clock timeout) and
-//      reads the new prices with sc1 loads.
-// Every polled word is zeroed by a memset ahead of each launch; epochs are period
-// indices within the launch.  Partial sums are combined in fixed order, so histories
-// are reproducible run to run (they differ from the per-period kernel's only in the
-// summation order of the mean, ~1e-16 relative).
+//   1. lookups: every lane carries NA agents (i = base + k TH + lane: consecutive lanes,
+//      consecutive agents) through m = R a + W l, c = cFunc[4 l + 2 Mrkv + 1](m, M)
+//      (merged-table lookup, panel_common.h), a = m - c in lock step, so a whole slice is
+//      in flight in one or two passes; partial sum of a in fixed order;
+//   2. publish: lane 0 stores the workgroup partial as two tagged 8-byte granules;
+//   3. next period's labour draws (Philox + inverse CDF, AS:1253-1254) do not depend on
+//      prices, so they run while the partials travel;
+//   4. wave 0 sweeps every workgroup's granules (relaxed agent-scope loads, s_sleep,
+//      wall-clock timeout), sums them in fixed order and runs calc_R_and_W
+//      (AS:1867-1894) -- every workgroup computes the same prices, no broadcast hop.
+// Granule slots alternate by period parity and are tagged with the period index
+// within the launch; they are zeroed by a memset ahead of each launch.  Partial sums
+// are combined in fixed order, so histories are reproducible run to run (they differ
+// from the per-period kernel's only in the summation order of the mean, ~1e-16
+// relative).
 #include "common.h"
 #include "internal.h"
 #include "panel_common.h"
@@ -33,8 +32,7 @@
 
 namespace aiy {
 
-constexpr int kResThreads = 1024;
-constexpr int kResMaxBlocks = 512;             // granule sweep: 16 granules per lane of one wave
+constexpr int kResMaxBlocks = 256;             // granule sweep: 8 granules per lane of one wave
 constexpr int kResGranPerLane = 2 * kResMaxBlocks / kWave;
 constexpr size_t kResLdsBudget = 150 * 1024;   // dynamic LDS per workgroup
 constexpr size_t kResHdrMaxBytes = 32 * 1024;  // row-header table in LDS
@@ -57,8 +55,6 @@ struct ResRun {
   unsigned* tmo;            // timeout word, zeroed
   double* hist_A;
   double* hist_M;
-  int sort_len;             // SORT: power of two >= chunk
-  int rotate;               // start each workgroup's sweep at a different slice offset
 };
 
 __device__ __forceinline__ int draw_labour(const double* s_cdf, int n_lab, int l0, double u) {
@@ -91,46 +87,26 @@ __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long lon
 }
 
 
-constexpr int kResResort = 32;   // SORT: periods between re-sorts of a slice
-
-// Ascending bitonic sort of (A, perm) in LDS, n a power of two; ties by perm (stable
-// and reproducible).  Ends with a barrier.
-__device__ __forceinline__ void bitonic_sort(double* A, unsigned short* perm, int n) {
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const double a0 = A[i], a1 = A[ixj];
-          const unsigned short p0 = perm[i], p1 = perm[ixj];
-          const bool gt = a0 > a1 || (a0 == a1 && p0 > p1);
-          if (((i & k) == 0) == gt) {
-            A[i] = a1; A[ixj] = a0;
-            perm[i] = p1; perm[ixj] = p0;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // Dynamic LDS: [cell headers (16-aligned)] [a: chunk doubles] [lab: chunk bytes]
 __host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
   return ((size_t)n_cells * sizeof(CellHdr) + 15) / 16 * 16;
 }
 
-template <bool IN_LDS, int kResA, bool SORT>
-__global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
+template <int TH, int NA, bool IN_LDS>
+__global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
   extern __shared__ __attribute__((aligned(16))) char s_dyn[];
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
-  __shared__ double s_red[kResThreads / kWave];
+  __shared__ double s_red[TH / kWave];
   __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
   __shared__ int s_abort;         // sweep timeout
+#ifdef AIY_DIAG_PHASES
+  __shared__ unsigned long long s_wdiag[TH / kWave];   // per-wave cycles inside tab_policy
+  if (threadIdx.x < TH / kWave) s_wdiag[threadIdx.x] = 0;
+#endif
 
   const int tid = threadIdx.x;
-  const int nthr = blockDim.x;
+  const int nthr = TH;
   const int nb = gridDim.x;
   const int n_M = P.n_M, n_lab = P.n_lab, n_J = P.tab.g.n_J, n_cells = P.tab.g.n_cells;
   const long long start = (long long)blockIdx.x * r.chunk;
@@ -138,31 +114,18 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
   CellHdr* hdr = reinterpret_cast<CellHdr*>(s_dyn);   // [cell]
   double* A;
   uint8_t* L;
-  unsigned short* perm = nullptr;    // SORT: agent (slice index) at sorted position k
-  const int P2 = SORT ? (int)r.sort_len : 0;
-  if constexpr (SORT) {
-    A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_cells));
-    perm = reinterpret_cast<unsigned short*>(A + P2);
-    L = reinterpret_cast<uint8_t*>(perm + P2);
-  } else if constexpr (IN_LDS) {
+  if constexpr (IN_LDS) {
     A = reinterpret_cast<double*>(s_dyn + res_hdr_bytes(n_cells));
     L = reinterpret_cast<uint8_t*>(A + r.chunk);
   } else {
     A = r.a + start;
     L = r.lab + start;
   }
-  const int rot = r.rotate ? (int)(((long long)blockIdx.x * cnt) / nb) : 0;
 
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = P.lab_cdf[q];
   for (int q = tid; q < n_lab; q += nthr) s_lvl[q] = P.lab_level[q];
   for (int q = tid; q < n_cells; q += nthr) hdr[q] = cell_header(P.tab, q);
-  if constexpr (SORT) {
-    for (int i = tid; i < P2; i += nthr) {
-      A[i] = i < cnt ? r.a[start + i] : __builtin_inf();
-      perm[i] = (unsigned short)i;
-      if (i < cnt) L[i] = r.lab[start + i];
-    }
-  } else if constexpr (IN_LDS) {
+  if constexpr (IN_LDS) {
     for (int i = tid; i < cnt; i += nthr) {
       A[i] = r.a[start + i];
       L[i] = r.lab[start + i];
@@ -186,12 +149,6 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
 #endif
   for (int p = 0; p < r.n_periods; ++p) {
     const int t = r.t0 + p;
-    if constexpr (SORT) {
-      if (p % kResResort == 0) {
-        __syncthreads();
-        bitonic_sort(A, perm, P2);   // agents by wealth: neighbouring lanes share policy lines
-      }
-    }
     const double Mnow = s_price[0], Rnow = s_price[1], Wnow = s_price[2];
     const int Mrkv = (int)s_price[3];
     int jc;
@@ -202,45 +159,50 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
 
     // ---- 1. agents: lookups, a = m - c, partial sum ----
     double local = 0.0;
-    for (int g0 = tid * kResA; g0 < cnt; g0 += nthr * kResA) {
-      double m[kResA];
-      int ln[kResA];
-      int pos[kResA];
+    for (int base = 0; base < cnt; base += TH * NA) {
+      double m[NA];
+      int ln[NA], cell[NA];
 #pragma unroll
-      for (int k = 0; k < kResA; ++k) {
-        int i = g0 + k < cnt ? g0 + k : cnt - 1;
-        if (rot) { i += rot; i = i >= cnt ? i - cnt : i; }
-        pos[k] = i;
-        ln[k] = SORT ? L[perm[i]] : L[i];
-        m[k] = Rnow * A[i] + Wnow * (s_lvl[ln[k]] * 1.0);                                   // AS:1283
+      for (int k = 0; k < NA; ++k) {
+        const int i0 = base + k * TH + tid;
+#ifdef AIY_DIAG_QUAD_DUP
+        const int i = (i0 < cnt ? i0 : cnt - 1) & ~3;   // diagnostic build only: 4 lanes, one agent
+#else
+        const int i = i0 < cnt ? i0 : cnt - 1;                                            // tail lanes: dummy work
+#endif
+        ln[k] = L[i];
+        m[k] = Rnow * A[i] + Wnow * (s_lvl[ln[k]] * 1.0);                                 // AS:1283
+        cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                          // employed (Urate = 0)
       }
 #ifdef AIY_DIAG_NO_LOOKUP
 #pragma unroll
-      for (int k = 0; k < kResA; ++k)
-        if (g0 + k < cnt) { A[pos[k]] = 0.9 * m[k]; local += 0.9 * m[k]; }   // diagnostic build only
+      for (int k = 0; k < NA; ++k) {
+        const int i = base + k * TH + tid;
+        if (i < cnt) { A[i] = 0.9 * m[k]; local += 0.9 * m[k]; }   // diagnostic build only
+      }
       continue;
 #endif
-      int cell[kResA];
-      CellHdr hh[kResA];
-#pragma unroll
-      for (int k = 0; k < kResA; ++k) {
-        cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                           // employed (Urate = 0)
-        hh[k] = hdr[cell[k]];
+      double c[NA];
+#ifdef AIY_DIAG_PHASES
+      const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
+      tab_policy<NA>(P.tab, cell, hdr, cell, m, alpha, n_M > 1, c);                       // AS:1326-1408
+#ifdef AIY_DIAG_PHASES
+      if ((tid & (kWave - 1)) == 0) {
+        const unsigned long long w1 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&s_wdiag[tid / kWave], (unsigned long long)(w1 - w0));
       }
-      double c[kResA];
-#ifdef AIY_DIAG_SAME_Q
-      double mq[kResA];   // diagnostic build only: every agent looks up the same query
-#pragma unroll
-      for (int k = 0; k < kResA; ++k) mq[k] = 2.0 + 1e-9 * k;
-      tab_policy<kResA>(P.tab, cell, hh, mq, alpha, n_M > 1, c);
-#else
-      tab_policy<kResA>(P.tab, cell, hh, m, alpha, n_M > 1, c);                             // AS:1326-1408
 #endif
 #pragma unroll
-      for (int k = 0; k < kResA; ++k) {
-        if (g0 + k < cnt) {
-          const double an = m[k] - c[k];                                                    // AS:1415
-          A[pos[k]] = an;
+      for (int k = 0; k < NA; ++k) {
+        const int i = base + k * TH + tid;
+#ifdef AIY_DIAG_QUAD_DUP
+        if (i < cnt && (i & 3) == 0) {
+#else
+        if (i < cnt) {
+#endif
+          const double an = m[k] - c[k];                                                  // AS:1415
+          A[i] = an;
           local += an;
         }
       }
@@ -315,12 +277,7 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
     if (s_abort) return;   // sweep timeout: the host reports it (tmo word)
     AIY_PH(4);
   }
-  if constexpr (SORT) {
-    for (int k = tid; k < cnt; k += nthr) {
-      r.a[start + perm[k]] = A[k];
-      r.lab[start + k] = L[k];
-    }
-  } else if constexpr (IN_LDS) {
+  if constexpr (IN_LDS) {
     for (int i = tid; i < cnt; i += nthr) {
       r.a[start + i] = A[i];
       r.lab[start + i] = L[i];
@@ -328,9 +285,16 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
   }
 #ifdef AIY_DIAG_PHASES
   if (tid == 0 && (blockIdx.x == 0 || blockIdx.x == nb / 2 || blockIdx.x == nb - 1))
+  {
     printf("[phases] block %d/%d cnt %d: lookup %.2f publish+draw %.2f sweep %.2f tail %.2f us/period\n", blockIdx.x, nb,
            cnt, ph[0] * 0.01 / r.n_periods, ph[1] * 0.01 / r.n_periods, ph[2] * 0.01 / r.n_periods,
            ph[3] * 0.01 / r.n_periods);
+    if (blockIdx.x == 0) {
+      for (int w = 0; w < TH / kWave; ++w)
+        printf("[phases] block 0 wave %d: tab_policy %.0f cycles/period\n", w, (double)s_wdiag[w] / r.n_periods);
+      printf("[phases] search-loop wave trips (all blocks) %u\n", diag_search_iters);
+    }
+  }
 #endif
   if (blockIdx.x == 0 && tid == 0 && r.n_periods > 0) {
     r.sow[0] = last.Mnow;
@@ -343,34 +307,33 @@ __global__ __launch_bounds__(kResThreads) void sim_resident_kernel(PanelDev P, R
   }
 }
 
+// Workgroup shape (threads per workgroup, agents per lane per pass) by handle option:
+// 0 -> 512 x 8 (default: a ~4k-agent slice in ONE pass, 256 VGPRs), 1 -> 1024 x 4.
+struct ResShape {
+  int th, na;
+};
+static ResShape res_shape(const aiy_handle* h) { return h->res_shape == 1 ? ResShape{1024, 4} : ResShape{512, 8}; }
+
 struct ResGeometry {
   int nb = 0;
   long long chunk = 0;
   bool in_lds = false;
   size_t lds = 0;
-  int sort_len = 0;
-  bool can_sort = false;
-  size_t lds_sort = 0;
 };
 
-static ResGeometry res_geometry(aiy_handle* h, long long n, int n_cells) {
+static ResGeometry res_geometry(aiy_handle* h, long long n, int n_cells, const ResShape& sh) {
   ResGeometry G;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) cus = 1;
-  const long long want = (n + 4095) / 4096;          // >= ~4 agents per lane
+  const long long want = (n + sh.th - 1) / sh.th;      // >= one agent per lane
   G.nb = (int)std::max(1LL, std::min<long long>(std::min(cus, kResMaxBlocks), want));
   G.chunk = (n + G.nb - 1) / G.nb;
-  G.chunk += G.chunk & 1;                            // even: Philox pairs never straddle workgroups
+  G.chunk += G.chunk & 1;                              // even: Philox pairs never straddle workgroups
   G.nb = (int)((n + G.chunk - 1) / G.chunk);
   const size_t hdr = res_hdr_bytes(n_cells);
   const size_t agents = (size_t)G.chunk * (sizeof(double) + 1);
   G.in_lds = hdr + agents <= kResLdsBudget;
   G.lds = G.in_lds ? (hdr + agents + 15) / 16 * 16 : hdr;
-  G.sort_len = 1;
-  while (G.sort_len < G.chunk) G.sort_len <<= 1;
-  const size_t sorted = hdr + (size_t)G.sort_len * (sizeof(double) + sizeof(unsigned short)) + G.chunk;
-  G.can_sort = G.sort_len <= 65536 && sorted <= kResLdsBudget;
-  G.lds_sort = (sorted + 15) / 16 * 16;
   return G;
 }
 
@@ -388,16 +351,15 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
                         int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
   if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
-  const ResGeometry G = res_geometry(h, n, P.tab.g.n_cells);
+  const ResShape sh = res_shape(h);
+  const ResGeometry G = res_geometry(h, n, P.tab.g.n_cells, sh);
   int32_t rc = ensure_res_scratch(h);
   if (rc) return rc;
-  const void* kernels[3][2] = {
-      {reinterpret_cast<const void*>(sim_resident_kernel<false, 2, false>),
-       reinterpret_cast<const void*>(sim_resident_kernel<false, 4, false>)},
-      {reinterpret_cast<const void*>(sim_resident_kernel<true, 2, false>),
-       reinterpret_cast<const void*>(sim_resident_kernel<true, 4, false>)},
-      {reinterpret_cast<const void*>(sim_resident_kernel<true, 2, true>),
-       reinterpret_cast<const void*>(sim_resident_kernel<true, 4, true>)}};
+  const void* kernels[2][2] = {
+      {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false>),
+       reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true>)},
+      {reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false>),
+       reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true>)}};
   static bool attr_set = false;
   if (!attr_set) {
     for (auto& row : kernels)
@@ -411,16 +373,12 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   r.gran = reinterpret_cast<unsigned long long*>(h->d_res_sync);
   r.tmo = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes);
   r.hist_A = hist_A; r.hist_M = hist_M;
-  r.sort_len = G.sort_len; r.rotate = h->res_order == 2 ? 1 : 0;
   PanelDev Pc = P;
   aiy_market mkc = mk;
   AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
-  const bool sort = h->res_order > 0 && G.can_sort;
-  const int variant = sort ? 2 : (G.in_lds ? 1 : 0);
-  const void* fn = kernels[variant][h->res_agents == 4 ? 1 : 0];
-  AIY_HIP(h, hipLaunchCooperativeKernel(fn, dim3(G.nb), dim3(kResThreads), args,
-                                        (unsigned)(sort ? G.lds_sort : G.lds), st));
+  const void* fn = kernels[sh.th == 1024 ? 1 : 0][G.in_lds ? 1 : 0];
+  AIY_HIP(h, hipLaunchCooperativeKernel(fn, dim3(G.nb), dim3(sh.th), args, (unsigned)G.lds, st));
   return AIY_OK;
 }
 

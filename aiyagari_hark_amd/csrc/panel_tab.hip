@@ -98,7 +98,6 @@ __global__ __launch_bounds__(256) void tab_index_kernel(PanelTabGeom g, char* __
     const long long b = (long long)((unsigned long long)__double_as_longlong(v) >> g.shift) - bk;
     return b > g.buckets - 1 ? g.buckets - 1 : (b < -1 ? -1 : b);
   };
-  const int t = brk_low_shift(g.shift);
   if (i < n) {
     const long long hi = c(i);
     const long long lo = (i == 0) ? -1 : c(i - 1);
@@ -106,7 +105,14 @@ __global__ __launch_bounds__(256) void tab_index_kernel(PanelTabGeom g, char* __
     if (hi > lo && hi >= 0) {
       int cnt = 1;
       while (cnt < BrkIdx::kCntSat && i + cnt < n && c(i + cnt) == hi) ++cnt;
-      E[hi] = brk_encode(i, cnt, (unsigned long long)__double_as_longlong(z[i]) >> t);
+      unsigned long long fields = 0;
+      if (cnt <= 3) {   // top w within-bucket bits of each node (brk_decode)
+        const int w = brk_field_bits(cnt, g.shift);
+        const unsigned long long mask = (1ull << w) - 1;
+        for (int j = 0; j < cnt; ++j)
+          fields |= ((((unsigned long long)__double_as_longlong(z[i + j])) >> (g.shift - w)) & mask) << (j * w);
+      }
+      E[hi] = brk_encode(i, cnt, fields);
     }
   } else {
     const long long last = c(n - 1);

@@ -231,10 +231,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 #define AIY_OPT_RESIDENT 2   /* value != 0 (default): single-rank panels of >= 65536 agents run
                                  a block of periods as ONE persistent launch (agents resident in
                                  LDS, in-kernel exchange of partial sums per period); 0: one launch
-                                 per period; 2 or 4: persistent, with that many agents per lane */
-#define AIY_OPT_RESIDENT_ORDER 3 /* persistent panel sweep order: 0 slice order (default), 1 agents
-                                    re-sorted by wealth every 32 periods, 2 sorted + per-workgroup
-                                    rotated start (results equal up to the summation order) */
+                                 per period */
+#define AIY_OPT_RESIDENT_SHAPE 3 /* persistent panel workgroup: 0 (default) 512 threads x 8 agents
+                                    per lane per pass, 1: 1024 threads x 4 (results identical) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

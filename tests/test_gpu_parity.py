@@ -169,8 +169,8 @@ def test_panel_philox_stream_matches_oracle(gpu, engine):
     assert np.array_equal(p.lab.cpu().numpy(), lab)
 
 
-@pytest.mark.parametrize("mode,order", [("philox", 0), ("numpy", 0), ("philox", 1), ("philox", 2)])
-def test_resident_panel_equals_per_period_kernel(gpu, mode, order):
+@pytest.mark.parametrize("mode,shape", [("philox", 0), ("numpy", 0), ("philox", 1)])
+def test_resident_panel_equals_per_period_kernel(gpu, mode, shape):
     """The persistent panel (one launch, agents in LDS, in-kernel grid barrier) against
     the one-launch-per-period kernel on 131 075 agents (odd: ragged last workgroup):
     labour states exact, assets (relative to the panel's scale) / history / market state
@@ -184,7 +184,7 @@ def test_resident_panel_equals_per_period_kernel(gpu, mode, order):
     U = rng.random((T, N))
     h = _lib.handle(gpu.index)
     out = {}
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, order), "aiy_set_option")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, shape), "aiy_set_option")
     for resident in (1, 0):
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, resident), "aiy_set_option")
         try:
@@ -210,7 +210,7 @@ def test_resident_panel_equals_per_period_kernel(gpu, mode, order):
                              p.sow.cpu().numpy())
         finally:
             h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, 1), "aiy_set_option")
-            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, 0), "aiy_set_option")
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, 0), "aiy_set_option")
     res, ref = out[1], out[0]
     assert np.array_equal(res[0], ref[0])
     # assets near the borrowing limit come out of a cancellation (a = m - c), so they are
@@ -356,7 +356,6 @@ def _brk_window(E, shift, n_buckets, n, q):
     bits = int(np.float64(q).view(np.uint64))
     key = (bits >> shift) - base
     lo_of = lambda e: int(e) >> 43  # noqa: E731
-    low = (1 << 40) - 1
     if not q > 0 or key < 0:
         return 0, lo_of(E[0])
     if key >= n_buckets - 1:
@@ -367,13 +366,14 @@ def _brk_window(E, shift, n_buckets, n, q):
     lo, cnt = lo_of(e), (e >> 40) & 7
     if cnt == 0:
         return lo, lo
-    if cnt == 1:
-        t = max(shift - 40, 0)
-        xs, qs = e & low, (bits >> t) & low
-        if xs != qs:
-            i = lo + (1 if xs < qs else 0)
-            return i, i
-        return (lo, lo) if t == 0 else (lo, lo + 1)
+    if cnt <= 3:
+        w = min(40 // cnt, shift)
+        mask = (1 << w) - 1
+        qf = (bits >> (shift - w)) & mask
+        xf = [(e >> (j * w)) & mask for j in range(cnt)]
+        below = sum(x < qf for x in xf)
+        upto = sum(x <= qf for x in xf)
+        return (lo + below, lo + below) if w == shift else (lo + below, lo + upto)
     return (lo, lo + cnt) if cnt < 7 else (lo, lo_of(E[key + 1]))
 
 
@@ -453,7 +453,7 @@ def test_panel_tables_semantics(gpu, name):
             assert np.array_equal(rec[cell, k], want), (cell, q, k)
     # random queries: at config-2 density most lookups resolve from the entry alone (at
     # N_a = 32 the two rows' nodes sit close together and often share a bucket)
-    assert resolved > (0.8 if name == "big" else 0.2) * total
+    assert resolved > (0.95 if name == "big" else 0.5) * total
 
 
 def test_stationary_capital_supply_matches_oracle(gpu):

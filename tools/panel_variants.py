@@ -49,8 +49,8 @@ def child(lib, opts):
         bench.run_step(econ, agent, bench.Probe())
         bench_panel = agent.panel
     for (res, agents, order, presort, Tt) in opts:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res if res == 0 else agents), "opt")
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_ORDER, order), "opt")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res), "opt")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, order), "opt")
         if bench_panel is not None:
             p = bench_panel
             a0, l0, s0 = p.a.clone(), p.lab.clone(), p.sow.clone()
@@ -95,9 +95,9 @@ def main():
         return
     variants = os.environ.get("AIY_VARIANTS", "")
     libs = [("default", None)] + [tuple(v.split("=", 1)) for v in variants.split(",") if v]
-    opts_all = [(1, 2, 0, 0, 400), (1, 4, 0, 0, 400), (1, 2, 1, 0, 400), (1, 2, 2, 0, 400), (0, 2, 0, 0, 400),
-                (1, 2, 0, 0, 50), (1, 2, 0, 1, 50), (1, 2, 0, 1, 10), (1, 2, 0, 1, 400)]
-    opts_var = [(1, 2, 0, 0, 400)]
+    # (resident, unused, resident shape, presort, periods)
+    opts_all = [(1, 0, 0, 0, 400), (1, 0, 1, 0, 400), (0, 0, 0, 0, 400), (1, 0, 0, 0, 50), (1, 0, 0, 1, 50)]
+    opts_var = [(1, 0, 0, 0, 400)]
     for name, lib in libs:
         opts = opts_all if lib is None else opts_var
         rc = subprocess.run([sys.executable, __file__, "--child", lib or "-", json.dumps(opts)], timeout=300).returncode
