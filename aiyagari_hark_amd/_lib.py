@@ -79,6 +79,8 @@ SIGNATURES = {
     "aiy_sim_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                              vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), vp]),
+    "aiy_panel_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64),
+                                                ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
     "aiy_sim_block_max_agents": (ctypes.c_int32, []),
     "aiy_sim_block_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelBatch), vp, ctypes.c_int64, vp, vp, vp,
                                                vp, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,

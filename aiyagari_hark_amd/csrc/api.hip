@@ -37,6 +37,8 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
   if (h->d_blk) (void)hipFree(h->d_blk);
   if (h->d_res_sync) (void)hipFree(h->d_res_sync);
+  for (hipEvent_t e : h->res_ev)
+    if (e) (void)hipEventDestroy(e);
   if (h->h_blk) (void)hipHostFree(h->h_blk);
   if (h->d_hdist) (void)hipFree(h->d_hdist);
   if (h->d_K) (void)hipFree(h->d_K);

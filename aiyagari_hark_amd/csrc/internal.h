@@ -43,6 +43,9 @@ struct aiy_handle {
   void* d_res_sync = nullptr;
   bool use_resident = true;
   int res_shape = 0;                 // resident workgroup shape: 0 = 512 threads x 8 agents, 1 = 1024 x 4
+  hipEvent_t res_ev[2] = {nullptr, nullptr};   // bracket every resident launch (aiy_panel_launch_stats)
+  double res_ms_sum = 0.0;
+  long long res_launches = 0, res_periods = 0;
   // block panel: per-calibration markets + seeds (device + pinned staging)
   void* d_blk = nullptr;
   void* h_blk = nullptr;

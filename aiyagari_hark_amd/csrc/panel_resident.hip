@@ -343,6 +343,8 @@ static int32_t ensure_res_scratch(aiy_handle* h) {
   if (!h->d_res_sync) {
     AIY_HIP(h, hipMalloc((void**)&h->d_res_sync, kResSyncBytes));
   }
+  for (hipEvent_t& e : h->res_ev)
+    if (!e) AIY_HIP(h, hipEventCreate(&e));
   return AIY_OK;
 }
 
@@ -378,7 +380,17 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
   const void* fn = kernels[sh.th == 1024 ? 1 : 0][G.in_lds ? 1 : 0];
-  AIY_HIP(h, hipLaunchCooperativeKernel(fn, dim3(G.nb), dim3(sh.th), args, (unsigned)G.lds, st));
+  // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
+  // against the occupancy query; a plain launch then has the same residency as a
+  // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),
+  // and the in-kernel sweep is bounded by a wall-clock timeout either way.
+  int per_cu = 0;
+  AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, sh.th, G.lds));
+  if (per_cu < 1) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: workgroup does not fit a CU");
+  AIY_HIP(h, hipEventRecord(h->res_ev[0], st));
+  AIY_HIP(h, hipLaunchKernel(fn, dim3(G.nb), dim3(sh.th), args, G.lds, st));
+  AIY_HIP(h, hipEventRecord(h->res_ev[1], st));
+  h->res_periods += n_periods;
   return AIY_OK;
 }
 
@@ -389,8 +401,29 @@ int32_t resident_status(aiy_handle* h, hipStream_t st) {
   AIY_HIP(h, hipMemcpyAsync(&tmo, reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes, sizeof(unsigned),
                             hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipStreamSynchronize(st));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, h->res_ev[0], h->res_ev[1]) == hipSuccess) {
+    h->res_ms_sum += ms;
+    h->res_launches += 1;
+  }
   if (tmo) return fail(h, AIY_ERR_STATE, "resident panel: partial-sum exchange timed out (workgroups not co-resident?)");
   return AIY_OK;
 }
 
 }  // namespace aiy
+
+// Launch statistics of the persistent panel (bench.py): kernel milliseconds summed over
+// the resident launches since the last reset, their number and the periods they ran.
+extern "C" int32_t aiy_panel_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, int64_t* periods,
+                                          int32_t reset) {
+  if (!h) return AIY_ERR_ARG;
+  if (ms_sum) *ms_sum = h->res_ms_sum;
+  if (launches) *launches = h->res_launches;
+  if (periods) *periods = h->res_periods;
+  if (reset) {
+    h->res_ms_sum = 0.0;
+    h->res_launches = 0;
+    h->res_periods = 0;
+  }
+  return AIY_OK;
+}

@@ -120,8 +120,10 @@ def run_step(econ, agent, probe: Probe):
         econ.solve_agents, econ.make_history = solve_agents, make_history
 
 
-def panel_kernel_time(agent, econ, n_launch=200):
-    """Average duration of the per-period panel kernel: HIP events on its stream."""
+def panel_kernel_time(agent, n_periods):
+    """Duration of ONE persistent panel launch covering a whole history of n_periods
+    periods (the launch aiy_sim_periods makes for make_history), from the end-of-history
+    population: HIP events on the launch's stream (aiy_sim_kernel_time)."""
     from aiyagari_hark_amd import _lib
     p = agent.panel
     h = _lib.handle(agent.device.index)
@@ -131,12 +133,11 @@ def panel_kernel_time(agent, econ, n_launch=200):
     pm, mk = p._model[:2]
     ms = ctypes.c_float()
     stream = torch.cuda.current_stream()
-    # warm
-    h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), p.n_local, _lib.ptr(a), _lib.ptr(lab),
-                                      99, 7, _lib.ptr(sow), 10, ctypes.byref(ms), stream.cuda_stream), "timing")
-    h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), p.n_local, _lib.ptr(a), _lib.ptr(lab),
-                                      99, 7, _lib.ptr(sow), n_launch, ctypes.byref(ms), stream.cuda_stream), "timing")
-    return ms.value / n_launch
+    for n in (10, n_periods):   # warm, then the timed history launch
+        h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), p.n_local, _lib.ptr(a),
+                                          _lib.ptr(lab), 99, 7, _lib.ptr(sow), n, ctypes.byref(ms),
+                                          stream.cuda_stream), "timing")
+    return ms.value
 
 
 def egm_kernel_time(agent, n_launch=20):
@@ -216,6 +217,8 @@ def main():
     ap.add_argument("--act-T", type=int, default=ACT_T)
     ap.add_argument("--t-discard", type=int, default=T_DISCARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-diag", action="store_true",
+                    help="skip the extra timing launches after the timed region (PMC passes)")
     args = ap.parse_args()
 
     world, rank, local = setup_dist()
@@ -230,12 +233,18 @@ def main():
     for _ in range(args.warmup):
         run_step(econ, agent, Probe())
     probe = Probe()
+    from aiyagari_hark_amd import _lib
+    hnd = _lib.handle(dev.index)
+    hnd.check(hnd.lib.aiy_panel_launch_stats(hnd.h, None, None, None, 1), "stats reset")
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_step(econ, agent, probe)
     barrier(world)
     elapsed = time.perf_counter() - t0
+    st_ms, st_n, st_per = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+    hnd.check(hnd.lib.aiy_panel_launch_stats(hnd.h, ctypes.byref(st_ms), ctypes.byref(st_n), ctypes.byref(st_per), 1),
+              "stats")
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -250,11 +259,20 @@ def main():
     cyc = probe.cycles / max(1, probe.ge_iters)
 
     # ---- dominant-kernel rooflines (live HIP events) ----
-    t_panel_ms = panel_kernel_time(agent, econ)
-    t_egm_ms = egm_kernel_time(agent)
-    panel_bytes = PANEL_BYTES_PER_AGENT * args.agents
+    # panel: one launch = one history (act_T periods of every agent); algorithmic bytes
+    # 18 per agent-period; EGM: one launch = one cycle, 32 B per node
+    # the timed region's own history launches (HIP events around each launch)
+    t_launch_ms = st_ms.value / max(1, st_n.value)
+    per_launch = st_per.value / max(1, st_n.value)
+    t_panel_ms = t_launch_ms / max(1.0, per_launch)
+    if args.no_kernel_diag:
+        t_conv_ms, t_egm_ms = float("nan"), float("nan")
+    else:
+        t_conv_ms = panel_kernel_time(agent, args.act_T) / args.act_T   # converged-policy history, diagnostic
+        t_egm_ms = egm_kernel_time(agent)
+    panel_bytes = PANEL_BYTES_PER_AGENT * args.agents * per_launch
     egm_bytes = 32 * 28 * 15 * (args.grid + 1)
-    panel_gbs = panel_bytes / (t_panel_ms * 1e-3) / 1e9
+    panel_gbs = panel_bytes / (t_launch_ms * 1e-3) / 1e9
     egm_gbs = egm_bytes / (t_egm_ms * 1e-3) / 1e9
     panel_share = probe.panel_s / max(1e-9, probe.panel_s + probe.egm_s)
 
@@ -283,17 +301,16 @@ def main():
         "egm_cycles_per_ge_iteration": cyc,
         "time_share": {"panel": panel_share, "egm": 1 - panel_share},
         "result": {"r": r, "K_over_Y": KtoY, "saving_rate": econ.DeprFac * KtoY},
-        "roofline": {"kernel": "sim_period_kernel" if panel_share >= 0.5 else "egm_cycle_kernel",
-                     "bound": "hbm", "achieved": panel_gbs if panel_share >= 0.5 else egm_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (panel_gbs if panel_share >= 0.5 else egm_gbs) / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("sim_period_kernel" if panel_share >= 0.5 else "egm_cycle_kernel"),
-                     "algorithmic_bytes_per_launch": panel_bytes if panel_share >= 0.5 else egm_bytes,
-                     "avg_launch_ms": t_panel_ms if panel_share >= 0.5 else t_egm_ms},
-        "roofline_other": {"kernel": "egm_cycle_kernel" if panel_share >= 0.5 else "sim_period_kernel",
-                           "achieved": egm_gbs if panel_share >= 0.5 else panel_gbs, "unit": "GB/s",
-                           "frac": (egm_gbs if panel_share >= 0.5 else panel_gbs) / HBM_PEAK_GBS,
-                           "avg_launch_ms": t_egm_ms if panel_share >= 0.5 else t_panel_ms},
+        "roofline": {"kernel": "sim_resident_kernel", "bound": "hbm", "achieved": panel_gbs,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": panel_gbs / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("sim_resident_kernel"),
+                     "algorithmic_bytes_per_launch": panel_bytes, "avg_launch_ms": t_launch_ms,
+                     "launch": f"one history: {per_launch:.0f} periods x {args.agents} agents",
+                     "launches_timed": st_n.value, "us_per_period": 1e3 * t_panel_ms,
+                     "us_per_period_converged_policy": 1e3 * t_conv_ms},
+        "roofline_other": {"kernel": "egm_cycle_kernel", "bound": "hbm", "achieved": egm_gbs, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": egm_gbs / HBM_PEAK_GBS, "traffic": pmc_traffic("egm_cycle_kernel"),
+                           "algorithmic_bytes_per_launch": egm_bytes, "avg_launch_ms": t_egm_ms},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

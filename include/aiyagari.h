@@ -194,6 +194,13 @@ int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* model, const a
                             int64_t n_local, double* a, uint8_t* lab, uint64_t seed, uint32_t ge_iter,
                             double* sow, int32_t n_launch, float* ms_out, aiy_stream stream);
 
+/* Persistent-panel launch statistics (measurement hook): kernel milliseconds summed over
+ * the single-rank resident launches since the last reset (each bracketed by HIP events
+ * on its stream), the number of launches and the periods they simulated.  reset != 0
+ * zeroes the counters after reading them.  Host-only. */
+int32_t aiy_panel_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, int64_t* periods,
+                               int32_t reset);
+
 /* Batched small-population panel (Table II in the reference's Krusell-Smith mode: 350-700
  * agents per calibration, act_T = 11 000; AH:217-249).  One workgroup owns one
  * calibration: agents stay in registers for all n_periods, the per-period mean of `a`
