@@ -34,6 +34,7 @@ namespace aiy {
 
 constexpr int kResMaxBlocks = 256;             // granule sweep: 8 granules per lane of one wave
 constexpr int kResGranPerLane = 2 * kResMaxBlocks / kWave;
+constexpr int kResMaxM = 64;                   // aggregate-M nodes staged in LDS
 constexpr size_t kResLdsBudget = 150 * 1024;   // dynamic LDS per workgroup
 constexpr size_t kResHdrMaxBytes = 32 * 1024;  // row-header table in LDS
 constexpr unsigned long long kResTimeoutTicks = 400000000ull;  // 4 s of the 100 MHz wall clock
@@ -63,26 +64,38 @@ __device__ __forceinline__ int draw_labour(const double* s_cdf, int n_lab, int l
   return l;
 }
 
-// Labour states of period t for the slice (in place: lab(t-1) -> lab(t)).
+// Labour states of period t for the slice (in place: lab(t-1) -> lab(t)).  Each thread
+// draws kDrawGroup agent pairs at once: their Philox chains are independent, so they
+// overlap instead of running back to back (the draw sits on the critical path of the
+// workgroup that publishes last).
+constexpr int kDrawGroup = 4;
 __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long long start, int cnt, int t,
                                            const double* s_cdf, int n_lab) {
   const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
   const double* u = r.u ? r.u + (size_t)(t - r.t0) * r.u_ld + start : nullptr;
-  for (int q = threadIdx.x; 2 * q < cnt; q += blockDim.x) {
-    const int i = 2 * q;
-    double u0, u1;
-    if (u) {
-      u0 = u[i];
-      u1 = i + 1 < cnt ? u[i + 1] : 0.0;
-    } else {
+  const int nthr = blockDim.x;
+  for (int q0 = threadIdx.x; 2 * q0 < cnt; q0 += kDrawGroup * nthr) {
+    double u0[kDrawGroup], u1[kDrawGroup];
+#pragma unroll
+    for (int g = 0; g < kDrawGroup; ++g) {
+      const int i = 2 * (q0 + g * nthr);
+      if (u) {
+        u0[g] = i < cnt ? u[i] : 0.0;
+        u1[g] = i + 1 < cnt ? u[i + 1] : 0.0;
+      } else {
 #ifdef AIY_DIAG_NO_PHILOX
-      u0 = 0.37 + 1e-9 * (double)(i & 1023); u1 = 0.41 + 1e-9 * (double)(i & 1023);   // diagnostic build only
+        u0[g] = 0.37 + 1e-9 * (double)(i & 1023); u1[g] = 0.41 + 1e-9 * (double)(i & 1023);   // diagnostic build only
 #else
-      philox_uniform2(ctr0, (uint64_t)((r.offset + start + i) >> 1), r.seed, 0u, u0, u1);
+        philox_uniform2(ctr0, (uint64_t)((r.offset + start + i) >> 1), r.seed, 0u, u0[g], u1[g]);
 #endif
+      }
     }
-    L[i] = (uint8_t)draw_labour(s_cdf, n_lab, L[i], u0);
-    if (i + 1 < cnt) L[i + 1] = (uint8_t)draw_labour(s_cdf, n_lab, L[i + 1], u1);
+#pragma unroll
+    for (int g = 0; g < kDrawGroup; ++g) {
+      const int i = 2 * (q0 + g * nthr);
+      if (i < cnt) L[i] = (uint8_t)draw_labour(s_cdf, n_lab, L[i], u0[g]);
+      if (i + 1 < cnt) L[i + 1] = (uint8_t)draw_labour(s_cdf, n_lab, L[i + 1], u1[g]);
+    }
   }
 }
 
@@ -97,6 +110,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
   extern __shared__ __attribute__((aligned(16))) char s_dyn[];
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
+  __shared__ double s_Mg[kResMaxM];   // Mgrid: the period's M bracket search stays in LDS
   __shared__ double s_red[TH / kWave];
   __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
   __shared__ int s_abort;         // sweep timeout
@@ -124,6 +138,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = P.lab_cdf[q];
   for (int q = tid; q < n_lab; q += nthr) s_lvl[q] = P.lab_level[q];
+  for (int q = tid; q < n_M; q += nthr) s_Mg[q] = P.M_grid[q];
   for (int q = tid; q < n_cells; q += nthr) hdr[q] = cell_header(P.tab, q);
   if constexpr (IN_LDS) {
     for (int i = tid; i < cnt; i += nthr) {
@@ -153,7 +168,8 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     const int Mrkv = (int)s_price[3];
     int jc;
     double alpha;
-    m_bracket(P.M_grid, n_M, Mnow, jc, alpha);
+    m_bracket(s_Mg, n_M, Mnow, jc, alpha);
+    const int mrkv_next = P.mrkv_hist[t];   // read-only history: issued early, used by the sweep
     __syncthreads();   // this period's labour draws complete
     AIY_PH(0);
 
@@ -230,7 +246,6 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     AIY_PH(2);
     // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices ----
     if (tid < kWave) {
-      const int mrkv_next = P.mrkv_hist[t];
       unsigned long long gv[kResGranPerLane];
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       int ok = 1;
@@ -337,7 +352,9 @@ static ResGeometry res_geometry(aiy_handle* h, long long n, int n_cells, const R
   return G;
 }
 
-bool resident_supported(const PanelDev& P) { return res_hdr_bytes(P.tab.g.n_cells) <= kResHdrMaxBytes; }
+bool resident_supported(const PanelDev& P) {
+  return res_hdr_bytes(P.tab.g.n_cells) <= kResHdrMaxBytes && P.n_M <= kResMaxM;
+}
 
 static int32_t ensure_res_scratch(aiy_handle* h) {
   if (!h->d_res_sync) {
