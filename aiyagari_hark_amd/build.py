@@ -36,23 +36,35 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_rebuild():
+def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
+    if out == LIB and not force and not needs_rebuild():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    tmp = LIB + ".tmp"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
            "-I/opt/rocm/include"]
+    cmd += [f"-D{d}" for d in defines]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     cmd += ["-L/opt/rocm/lib", "-lrccl", "-o", tmp]
     if verbose:
         print("[aiyagari build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
+
+
+def build_variant(name: str, defines) -> str:
+    """Diagnostic / tuning build (tools/panel_variants.py): lib/variants/libaiyagari_<name>.so
+    with extra preprocessor defines; never loaded by the product path."""
+    return build(out=os.path.join(LIBDIR, "variants", f"libaiyagari_{name}.so"), defines=defines)
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    print(LIB)
+    # python -m aiyagari_hark_amd.build [--force] | --variant NAME DEFINE [DEFINE ...]
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:]))
+    else:
+        build(force="--force" in sys.argv)
+        print(LIB)

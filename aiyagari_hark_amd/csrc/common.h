@@ -173,59 +173,55 @@ __host__ __device__ __forceinline__ int brk_field_bits(int cnt, int shift) {
 }
 __device__ __forceinline__ int brk_lo(unsigned long long e) { return (int)(e >> 43); }
 
-// Bracket-index lookup in two steps, so callers can issue the entry load themselves
-// (e.g. as a buffer load) and keep many lookups in flight:
-//   brk_bucket: the entry to load (>= 0) or -1 when no entry load is needed; the rare
-//               cases (below the first bucket, capped top bucket) load here directly
-//               and leave [lo, hi) set.
-//   brk_decode: [lo, hi) from the loaded entry; lo == hi means the bracket is known.
-__device__ __forceinline__ long long brk_bucket(const unsigned long long* __restrict__ E, int shift, int buckets,
-                                                int base, int last, int n, double q, int& lo, int& hi) {
-  lo = 0;
-  hi = n;
-  if (base == kIdxNoBase) return -1;
-  const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
-  const long long key = (long long)(bits >> shift) - (long long)base;
-  if (!(q > 0.0) || key < 0) { lo = 0; hi = brk_lo(E[0]); return -1; }
-  if (key >= buckets - 1) {                             // capped top bucket / beyond the span
-    if (last == buckets - 1) { lo = brk_lo(E[buckets - 1]); hi = n; } else { lo = n; hi = n; }
-    return -1;
-  }
-  if (key > last) { lo = n; hi = n; return -1; }        // above every node
-  return key;
+// Bracket-index lookup in two branch-free steps, so callers issue the entry load
+// themselves (a buffer load) and keep many lookups in flight:
+//   brk_slot:    the entry to load -- always in [0, buckets): q below the first bucket
+//                (or q <= 0, NaN) loads E[0], q at or beyond the capped top bucket
+//                E[buckets - 1] -- and the raw bucket key for brk_resolve;
+//   brk_resolve: [lo, hi) from that entry; lo == hi means the lower bound is known,
+//                need_next that hi is brk_lo(E[slot + 1]) (a bucket of >= 7 nodes).
+// Every case is a select, so a wave decodes each lookup as soon as its entry arrives
+// (no branch, no wait for the other lookups in flight).  Below the first bucket the
+// window [0, E[0].lo) holds at most the two borrowing nodes z[0], z[1] (E[0].lo <= 2:
+// the base bucket is z[2]'s), so the lower bound is counted from them directly (z01 =
+// {z[0], z[1]}, held by the caller) -- the borrowing-constrained agents resolve without
+// a search step.
+__device__ __forceinline__ int brk_slot(int shift, int buckets, int base, double q, long long& raw) {
+  const long long k = (long long)((unsigned long long)__double_as_longlong(q) >> shift) - (long long)base;
+  raw = (q > 0.0) ? k : -1;
+  const long long c = raw < 0 ? 0 : (raw > buckets - 1 ? buckets - 1 : raw);
+  return (int)c;
 }
-__device__ __forceinline__ void brk_decode(const unsigned long long* __restrict__ E, int shift, int n, long long key,
-                                           unsigned long long e, double q, int& lo, int& hi) {
+__device__ __forceinline__ void brk_resolve(int shift, int buckets, int base, int last, int n, long long raw,
+                                            unsigned long long e, double q, double z0, double z1, int& lo, int& hi,
+                                            bool& need_next) {
   const unsigned long long bits = (unsigned long long)__double_as_longlong(q);
   const int l = brk_lo(e);
   const int c = (int)((e >> 40) & 7u);
-  if (c == 0) { lo = l; hi = l; }
-  else if (c <= 3) {
-    const int w = brk_field_bits(c, shift);
-    const unsigned long long mask = (1ull << w) - 1;
-    const unsigned long long qf = (bits >> (shift - w)) & mask;
-    int below = 0, upto = 0;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (j < c) {
-        const unsigned long long xf = (e >> (j * w)) & mask;
-        below += xf < qf ? 1 : 0;
-        upto += xf <= qf ? 1 : 0;
-      }
-    }
-    lo = l + below;                                       // nodes of the bucket below q
-    hi = (w == shift) ? lo : l + upto;                    // a tie in a truncated field: search it
+  const int w0 = c <= 1 ? 40 : (c == 2 ? 20 : 13);   // brk_field_bits for c = 1..3
+  const int w = w0 < shift ? w0 : shift;
+  const unsigned long long mask = (1ull << w) - 1;
+  const unsigned long long qf = (bits >> (shift - w)) & mask;
+  const unsigned long long f0 = e & mask, f1 = (e >> w) & mask, f2 = (e >> (2 * w)) & mask;
+  const int below = (f0 < qf ? 1 : 0) + (c >= 2 && f1 < qf ? 1 : 0) + (c >= 3 && f2 < qf ? 1 : 0);
+  const int upto = (f0 <= qf ? 1 : 0) + (c >= 2 && f1 <= qf ? 1 : 0) + (c >= 3 && f2 <= qf ? 1 : 0);
+  const bool fields = c >= 1 && c <= 3;
+  int nlo = fields ? l + below : l;
+  int nhi = fields ? (w == shift ? nlo : l + upto) : (c < BrkIdx::kCntSat ? l + c : l);
+  bool nx = c == BrkIdx::kCntSat;
+  if (raw < 0) {                                       // below the first bucket (E[0] loaded)
+    const int b = (l > 0 && z0 < q ? 1 : 0) + (l > 1 && z1 < q ? 1 : 0);
+    nlo = b; nhi = b; nx = false;
+    if (l > 2) { nlo = 0; nhi = l; }                   // not a table of ours: search the window
+  } else if (raw >= buckets - 1) {                     // capped top bucket (E[buckets - 1] loaded)
+    const bool capped = last == buckets - 1;
+    nlo = capped ? l : n; nhi = n; nx = false;
+  } else if (raw > last) {                             // above every node
+    nlo = n; nhi = n; nx = false;
   }
-  else if (c < BrkIdx::kCntSat) { lo = l; hi = l + c; }
-  else { lo = l; hi = brk_lo(E[key + 1]); }
-  if (lo < 0 || hi > n || lo > hi) { lo = 0; hi = n; }  // defensive: unsorted rows
-}
-
-// Search window [lo, hi) of lower_bound(x[0..n), q) from a bracket index.
-__device__ __forceinline__ void brk_window(const unsigned long long* __restrict__ E, int shift, int buckets, int base,
-                                           int last, int n, double q, int& lo, int& hi) {
-  const long long key = brk_bucket(E, shift, buckets, base, last, n, q, lo, hi);
-  if (key >= 0) brk_decode(E, shift, n, key, E[key], q, lo, hi);
+  if (base == kIdxNoBase) { nlo = 0; nhi = n; nx = false; }   // no positive node: full search
+  if (!nx && (nlo < 0 || nhi > n || nlo > nhi)) { nlo = 0; nhi = n; }   // defensive: unsorted rows
+  lo = nlo; hi = nhi; need_next = nx;
 }
 
 // Search window [lo, hi) of lower_bound(x[0..n), q) from the row index H (base given).

@@ -42,7 +42,7 @@ struct aiy_handle {
   // resident panel: tagged partial-sum granules + timeout word; option
   void* d_res_sync = nullptr;
   bool use_resident = true;
-  int res_shape = 0;                 // resident workgroup shape: 0 = 512 threads x 8 agents, 1 = 1024 x 4
+  int res_shape = 0;                 // resident workgroup shape (AIY_OPT_RESIDENT_SHAPE)
   hipEvent_t res_ev[2] = {nullptr, nullptr};   // bracket every resident launch (aiy_panel_launch_stats)
   double res_ms_sum = 0.0;
   long long res_launches = 0, res_periods = 0;

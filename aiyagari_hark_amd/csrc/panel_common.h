@@ -118,32 +118,91 @@ __device__ unsigned diag_search_iters;   // diagnostic build only: wave search-l
 // BLEND = false: one row (n_M == 1).  Every load is unconditional and BLEND is a
 // compile-time choice: a data-dependent branch between the loads makes the compiler
 // wait for each agent's record before issuing the next (measured: 8 serial round trips).
-template <int NA, bool BLEND>
+// Quad-cooperative record loads (QUAD = true; the four lanes of every quad must be
+// active).  The per-lane pattern -- four 16-byte loads of the lane's own record --
+// touches 64 cache lines per load instruction; here the quad loads one agent's record
+// per instruction (lane q the q-th 16-byte chunk: 16 lines per instruction, the same
+// instruction count) and a 4 x 4 transpose across the quad (two DPP exchange stages)
+// hands every lane its own record.  Measured at configs[1]: 23.3 -> 21.2 us per period.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = dpp_u32<CTRL>((unsigned)b), hi = dpp_u32<CTRL>((unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int CTRL>
+__device__ __forceinline__ double2 dpp_f64x2(double2 v) {
+  return make_double2(dpp_f64<CTRL>(v.x), dpp_f64<CTRL>(v.y));
+}
+__device__ __forceinline__ double2 sel2(bool p, double2 a, double2 b) {
+  return make_double2(p ? a.x : b.x, p ? a.y : b.y);
+}
+constexpr int kDppXor1 = 0xB1;   // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4E;   // quad_perm [2, 3, 0, 1]
+// t[r] = chunk q of agent r (lane q of the quad)  ->  t[c] = chunk c of agent q.
+__device__ __forceinline__ void quad_transpose(double2 (&t)[4], int q) {
+  const bool b0 = q & 1, b1 = q & 2;
+  const double2 x0 = dpp_f64x2<kDppXor1>(t[0]), x1 = dpp_f64x2<kDppXor1>(t[1]);
+  const double2 x2 = dpp_f64x2<kDppXor1>(t[2]), x3 = dpp_f64x2<kDppXor1>(t[3]);
+  const double2 a0 = sel2(b0, x1, t[0]), a1 = sel2(b0, t[1], x0);
+  const double2 a2 = sel2(b0, x3, t[2]), a3 = sel2(b0, t[3], x2);
+  const double2 y0 = dpp_f64x2<kDppXor2>(a0), y1 = dpp_f64x2<kDppXor2>(a1);
+  const double2 y2 = dpp_f64x2<kDppXor2>(a2), y3 = dpp_f64x2<kDppXor2>(a3);
+  t[0] = sel2(b1, y2, a0);
+  t[2] = sel2(b1, a2, y0);
+  t[1] = sel2(b1, y3, a1);
+  t[3] = sel2(b1, a3, y1);
+}
+
+template <int NA, bool BLEND, bool QUAD = false>
 __device__ __forceinline__ void tab_policy_t(const PanelTab& T, const int (&cell)[NA], const CellHdr* hdr,
                                              const int (&hidx)[NA], const double (&m)[NA], double alpha,
                                              double (&c)[NA]) {
   const PanelTabGeom& g = T.g;
   const __amdgpu_buffer_rsrc_t ridx = tab_rsrc(T.idx, (long long)g.n_cells * g.idx_stride * 8);
   const __amdgpu_buffer_rsrc_t rrec = tab_rsrc(T.rec, (long long)g.n_cells * g.rec_stride * 16);
-  int lo[NA], hi[NA];
-  long long key[NA];
+  int slot[NA], lo[NA], hi[NA];
+  long long raw[NA];
+  bool nx[NA];
 #pragma unroll
-  for (int k = 0; k < NA; ++k)
-    key[k] = brk_bucket(T.idx + (size_t)cell[k] * g.idx_stride, g.shift, g.buckets, hdr[hidx[k]].base,
-                        hdr[hidx[k]].last, g.Z, m[k], lo[k], hi[k]);
+  for (int k = 0; k < NA; ++k) slot[k] = brk_slot(g.shift, g.buckets, hdr[hidx[k]].base, m[k], raw[k]);
+#ifdef AIY_DIAG_NO_INDEX
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {   // diagnostic build only: record position from the bucket, no index load
+    lo[k] = hi[k] = (int)((long long)slot[k] * g.Z / g.buckets);
+    nx[k] = false;
+  }
+#else
   unsigned long long e[NA];
 #pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    const unsigned eo = (unsigned)(((long long)cell[k] * g.idx_stride + (key[k] >= 0 ? key[k] : 0)) * 8);
-    e[k] = buf_u64(ridx, eo);
-  }
+  for (int k = 0; k < NA; ++k) e[k] = buf_u64(ridx, (unsigned)(((long long)cell[k] * g.idx_stride + slot[k]) * 8));
 #pragma unroll
-  for (int k = 0; k < NA; ++k)
-    if (key[k] >= 0) brk_decode(T.idx + (size_t)cell[k] * g.idx_stride, g.shift, g.Z, key[k], e[k], m[k], lo[k], hi[k]);
+  for (int k = 0; k < NA; ++k) {
+    const CellHdr& H = hdr[hidx[k]];
+    const double z0 = H.first0 < H.first1 ? H.first0 : H.first1;
+    const double z1 = H.first0 < H.first1 ? H.first1 : H.first0;
+    brk_resolve(g.shift, g.buckets, H.base, H.last, g.Z, raw[k], e[k], m[k], z0, z1, lo[k], hi[k], nx[k]);
+  }
+#endif
+#ifdef AIY_DIAG_NO_RECORD
+#pragma unroll
+  for (int k = 0; k < NA; ++k) c[k] = 0.9 * m[k] + 1e-30 * lo[k];   // diagnostic build only: no record load
+  return;
+#endif
+  // Rare: buckets of >= 7 nodes (window to the end of z), truncated-field ties,
+  // degenerate tables -- binary search over z.  The common case falls through with no
+  // branch between the index trip and the record trip.
   bool more = false;
 #pragma unroll
-  for (int k = 0; k < NA; ++k) more = more || (lo[k] < hi[k]);
-  while (more) {   // buckets holding >= 2 merged nodes: binary search over z
+  for (int k = 0; k < NA; ++k) {
+    if (nx[k]) hi[k] = g.Z;
+    more = more || (lo[k] < hi[k]);
+  }
+  while (more) {
     more = false;
 #ifdef AIY_DIAG_PHASES
     if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(&diag_search_iters, 1u);
@@ -164,14 +223,36 @@ __device__ __forceinline__ void tab_policy_t(const PanelTab& T, const int (&cell
     }
   }
   double2 p0[NA], p1[NA], p2[NA], p3[NA];
+  if constexpr (QUAD && BLEND) {
+    const int q = (int)(threadIdx.x & 3);
+    const unsigned qo = 16u * (unsigned)q;
+    double2 t[NA][4];
 #pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    const unsigned off = (unsigned)(((long long)cell[k] * g.rec_stride + 4LL * lo[k]) * 16);
-    p0[k] = buf_f64x2(rrec, off, 0);
-    p1[k] = buf_f64x2(rrec, off, 16);
-    if constexpr (BLEND) {
-      p2[k] = buf_f64x2(rrec, off, 32);
-      p3[k] = buf_f64x2(rrec, off, 48);
+    for (int k = 0; k < NA; ++k) {
+      const unsigned off = (unsigned)(((long long)cell[k] * g.rec_stride + 4LL * lo[k]) * 16);
+      t[k][0] = buf_f64x2(rrec, dpp_u32<0x00>(off) + qo, 0);   // agent of quad lane 0
+      t[k][1] = buf_f64x2(rrec, dpp_u32<0x55>(off) + qo, 0);
+      t[k][2] = buf_f64x2(rrec, dpp_u32<0xAA>(off) + qo, 0);
+      t[k][3] = buf_f64x2(rrec, dpp_u32<0xFF>(off) + qo, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      quad_transpose(t[k], q);
+      p0[k] = t[k][0];
+      p1[k] = t[k][1];
+      p2[k] = t[k][2];
+      p3[k] = t[k][3];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const unsigned off = (unsigned)(((long long)cell[k] * g.rec_stride + 4LL * lo[k]) * 16);
+      p0[k] = buf_f64x2(rrec, off, 0);
+      p1[k] = buf_f64x2(rrec, off, 16);
+      if constexpr (BLEND) {
+        p2[k] = buf_f64x2(rrec, off, 32);
+        p3[k] = buf_f64x2(rrec, off, 48);
+      }
     }
   }
 #pragma unroll
@@ -192,12 +273,12 @@ __device__ __forceinline__ void tab_policy_t(const PanelTab& T, const int (&cell
   }
 }
 
-template <int NA>
+template <int NA, bool QUAD = false>
 __device__ __forceinline__ void tab_policy(const PanelTab& T, const int (&cell)[NA], const CellHdr* hdr,
                                            const int (&hidx)[NA], const double (&m)[NA], double alpha, bool blend,
                                            double (&c)[NA]) {
-  if (blend) tab_policy_t<NA, true>(T, cell, hdr, hidx, m, alpha, c);
-  else tab_policy_t<NA, false>(T, cell, hdr, hidx, m, alpha, c);
+  if (blend) tab_policy_t<NA, true, QUAD>(T, cell, hdr, hidx, m, alpha, c);
+  else tab_policy_t<NA, false, QUAD>(T, cell, hdr, hidx, m, alpha, c);
 }
 
 // The period's M bracket (LinearInterpOnInterp1D: clip(searchsorted(Mgrid, M), 1,

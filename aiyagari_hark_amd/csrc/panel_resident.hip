@@ -68,16 +68,18 @@ __device__ __forceinline__ int draw_labour(const double* s_cdf, int n_lab, int l
 // draws kDrawGroup agent pairs at once: their Philox chains are independent, so they
 // overlap instead of running back to back (the draw sits on the critical path of the
 // workgroup that publishes last).
+// Thread `vt` of `nvt` drawing threads takes agent pairs vt, vt + nvt, ..., G at a time.
 constexpr int kDrawGroup = 4;
+template <int G>
 __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long long start, int cnt, int t,
-                                           const double* s_cdf, int n_lab) {
+                                           const double* s_cdf, int n_lab, int vt, int nvt) {
   const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
   const double* u = r.u ? r.u + (size_t)(t - r.t0) * r.u_ld + start : nullptr;
-  const int nthr = blockDim.x;
-  for (int q0 = threadIdx.x; 2 * q0 < cnt; q0 += kDrawGroup * nthr) {
-    double u0[kDrawGroup], u1[kDrawGroup];
+  const int nthr = nvt;
+  for (int q0 = vt; 2 * q0 < cnt; q0 += G * nthr) {
+    double u0[G], u1[G];
 #pragma unroll
-    for (int g = 0; g < kDrawGroup; ++g) {
+    for (int g = 0; g < G; ++g) {
       const int i = 2 * (q0 + g * nthr);
       if (u) {
         u0[g] = i < cnt ? u[i] : 0.0;
@@ -91,7 +93,7 @@ __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long lon
       }
     }
 #pragma unroll
-    for (int g = 0; g < kDrawGroup; ++g) {
+    for (int g = 0; g < G; ++g) {
       const int i = 2 * (q0 + g * nthr);
       if (i < cnt) L[i] = (uint8_t)draw_labour(s_cdf, n_lab, L[i], u0[g]);
       if (i + 1 < cnt) L[i + 1] = (uint8_t)draw_labour(s_cdf, n_lab, L[i + 1], u1[g]);
@@ -105,7 +107,7 @@ __host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
   return ((size_t)n_cells * sizeof(CellHdr) + 15) / 16 * 16;
 }
 
-template <int TH, int NA, bool IN_LDS>
+template <int TH, int NA, bool IN_LDS, bool QUAD>
 __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
   extern __shared__ __attribute__((aligned(16))) char s_dyn[];
   __shared__ double s_cdf[kLdsLab * kLdsLab];
@@ -153,7 +155,8 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     s_price[3] = load_f64_agent(&r.sow[2]);
   }
   __syncthreads();
-  draw_slice(r, L, start, cnt, r.t0, s_cdf, n_lab);
+  draw_slice<kDrawGroup>(r, L, start, cnt, r.t0, s_cdf, n_lab, tid, TH);
+  __syncthreads();   // period t0's labour draws complete
 
   Prices last{};
 #ifdef AIY_DIAG_PHASES
@@ -170,7 +173,6 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     double alpha;
     m_bracket(s_Mg, n_M, Mnow, jc, alpha);
     const int mrkv_next = P.mrkv_hist[t];   // read-only history: issued early, used by the sweep
-    __syncthreads();   // this period's labour draws complete
     AIY_PH(0);
 
     // ---- 1. agents: lookups, a = m - c, partial sum ----
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #ifdef AIY_DIAG_PHASES
       const unsigned long long w0 = __builtin_amdgcn_s_memtime();
 #endif
-      tab_policy<NA>(P.tab, cell, hdr, cell, m, alpha, n_M > 1, c);                       // AS:1326-1408
+      tab_policy<NA, QUAD>(P.tab, cell, hdr, cell, m, alpha, n_M > 1, c);                       // AS:1326-1408
 #ifdef AIY_DIAG_PHASES
       if ((tid & (kWave - 1)) == 0) {
         const unsigned long long w1 = __builtin_amdgcn_s_memtime();
@@ -241,8 +243,23 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
       __hip_atomic_store(&gslot[2 * blockIdx.x + 1], ((unsigned long long)e << 32) | (bits & 0xffffffffull),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // ---- 3. next period's labour draws overlap the exchange ----
-    if (p + 1 < r.n_periods) draw_slice(r, L, start, cnt, t + 1, s_cdf, n_lab);
+    // ---- 3. next period's labour draws overlap the exchange (waves 1..; wave 0 sweeps) ----
+#ifndef AIY_DRAW_MODE
+#define AIY_DRAW_MODE 2
+#endif
+    if (p + 1 < r.n_periods) {
+#if AIY_DRAW_MODE == 0   // every wave draws, wave 0 then sweeps
+      draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid, TH);
+#elif AIY_DRAW_MODE == 1   // wave 4 takes wave 0's pairs
+      if (tid >= kWave) {
+        draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid, TH);
+        if (tid >= 4 * kWave && tid < 5 * kWave)
+          draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid - 4 * kWave, TH);
+      }
+#else   // waves 1.. share every pair
+      if (tid >= kWave) draw_slice<kDrawGroup + 1>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid - kWave, TH - kWave);
+#endif
+    }
     AIY_PH(2);
     // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices ----
     if (tid < kWave) {
@@ -301,7 +318,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #ifdef AIY_DIAG_PHASES
   if (tid == 0 && (blockIdx.x == 0 || blockIdx.x == nb / 2 || blockIdx.x == nb - 1))
   {
-    printf("[phases] block %d/%d cnt %d: lookup %.2f publish+draw %.2f sweep %.2f tail %.2f us/period\n", blockIdx.x, nb,
+    printf("[phases] block %d/%d cnt %d: lookup %.2f publish %.2f sweep %.2f prices+draws %.2f us/period\n", blockIdx.x, nb,
            cnt, ph[0] * 0.01 / r.n_periods, ph[1] * 0.01 / r.n_periods, ph[2] * 0.01 / r.n_periods,
            ph[3] * 0.01 / r.n_periods);
     if (blockIdx.x == 0) {
@@ -322,12 +339,19 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
   }
 }
 
-// Workgroup shape (threads per workgroup, agents per lane per pass) by handle option:
-// 0 -> 512 x 8 (default: a ~4k-agent slice in ONE pass, 256 VGPRs), 1 -> 1024 x 4.
+// Workgroup shape (threads per workgroup, agents per lane per pass, record loads) by
+// handle option: 0 -> 512 x 8 quad-cooperative (default: a ~4k-agent slice in ONE pass,
+// 256 VGPRs), 1 -> 1024 x 4 quad-cooperative, 2 -> 512 x 8 per-lane record loads.
 struct ResShape {
-  int th, na;
+  int id, th, na;
 };
-static ResShape res_shape(const aiy_handle* h) { return h->res_shape == 1 ? ResShape{1024, 4} : ResShape{512, 8}; }
+static ResShape res_shape(const aiy_handle* h) {
+  switch (h->res_shape) {
+    case 1: return ResShape{1, 1024, 4};
+    case 2: return ResShape{2, 512, 8};
+    default: return ResShape{0, 512, 8};
+  }
+}
 
 struct ResGeometry {
   int nb = 0;
@@ -374,11 +398,13 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   const ResGeometry G = res_geometry(h, n, P.tab.g.n_cells, sh);
   int32_t rc = ensure_res_scratch(h);
   if (rc) return rc;
-  const void* kernels[2][2] = {
-      {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false>),
-       reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true>)},
-      {reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false>),
-       reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true>)}};
+  const void* kernels[3][2] = {
+      {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true>),
+       reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, true>)},
+      {reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false, true>),
+       reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true>)},
+      {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false>),
+       reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false>)}};
   static bool attr_set = false;
   if (!attr_set) {
     for (auto& row : kernels)
@@ -396,7 +422,7 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   aiy_market mkc = mk;
   AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
-  const void* fn = kernels[sh.th == 1024 ? 1 : 0][G.in_lds ? 1 : 0];
+  const void* fn = kernels[sh.id][G.in_lds ? 1 : 0];
   // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
   // against the occupancy query; a plain launch then has the same residency as a
   // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),

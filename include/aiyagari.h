@@ -240,7 +240,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                  LDS, in-kernel exchange of partial sums per period); 0: one launch
                                  per period */
 #define AIY_OPT_RESIDENT_SHAPE 3 /* persistent panel workgroup: 0 (default) 512 threads x 8 agents
-                                    per lane per pass, 1: 1024 threads x 4 (results identical) */
+                                    per lane per pass, quad-cooperative record loads; 1: 1024
+                                    threads x 4, quad-cooperative; 2: 512 x 8, per-lane record
+                                    loads (results identical) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

@@ -169,7 +169,7 @@ def test_panel_philox_stream_matches_oracle(gpu, engine):
     assert np.array_equal(p.lab.cpu().numpy(), lab)
 
 
-@pytest.mark.parametrize("mode,shape", [("philox", 0), ("numpy", 0), ("philox", 1)])
+@pytest.mark.parametrize("mode,shape", [("philox", 0), ("numpy", 0), ("philox", 1), ("philox", 2)])
 def test_resident_panel_equals_per_period_kernel(gpu, mode, shape):
     """The persistent panel (one launch, agents in LDS, in-kernel grid barrier) against
     the one-launch-per-period kernel on 131 075 agents (odd: ragged last workgroup):

@@ -98,6 +98,8 @@ def main():
     # (resident, unused, resident shape, presort, periods)
     opts_all = [(1, 0, 0, 0, 400), (1, 0, 1, 0, 400), (0, 0, 0, 0, 400), (1, 0, 0, 0, 50), (1, 0, 0, 1, 50)]
     opts_var = [(1, 0, 0, 0, 400)]
+    if os.environ.get("OPTS"):
+        opts_all = opts_var = [tuple(o) for o in json.loads(os.environ["OPTS"])]
     for name, lib in libs:
         opts = opts_all if lib is None else opts_var
         rc = subprocess.run([sys.executable, __file__, "--child", lib or "-", json.dumps(opts)], timeout=300).returncode
