@@ -29,6 +29,7 @@ AIY_SOW_DOUBLES = 8
 AIY_OPT_USE_GRAPHS = 1
 AIY_OPT_RESIDENT = 2
 AIY_OPT_RESIDENT_SHAPE = 3
+AIY_OPT_HIST_FUSED = 4
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

@@ -160,6 +160,144 @@ __global__ __launch_bounds__(256) void hist_mix_kernel(int S, int n_a, const dou
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Fused lottery step (push + mix in one launch, no global atomics, no T buffer).
+// With a monotone savings policy lo[s][j] is non-decreasing in j, so the sources that
+// land in a destination tile [d0, d1) are one contiguous range per s:
+//   jb[s][d] = first j with lo[s][j] >= d   (hist_range_kernel, once per lottery)
+//   sources of the tile: j in [jb[s][d0 - 1], jb[s][d1])
+// One workgroup per (tile of kHistTile destinations, calibration): the tile's sources
+// of every s are flattened into one index space (adjacent lanes -> adjacent j, keys
+// (s, d) sorted), pushed with the same vlo = w m, vhi = (1 - w) m products as
+// hist_push_kernel through the segmented wave sum into LDS atomics, then mixed over s
+// exactly as hist_mix_kernel (same order of the S x S contraction, same distance and
+// sticky protocol).  HBM per point and iteration: lo 4 + w 8 + mass 8 + mass' 8 = 28 B
+// (the mass re-read of the distance hits L2).
+// ---------------------------------------------------------------------------------
+constexpr int kHistTile = 256;
+constexpr int kHistUnroll = 4;
+
+__global__ __launch_bounds__(256) void hist_range_kernel(int S, int n_a, const int* __restrict__ lo,
+                                                         int* __restrict__ jb, int* flag) {
+  const int cal = blockIdx.z, s = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > n_a) return;   // j == n_a closes the row: d in (lo[n_a - 1], n_a] -> n_a
+  const size_t r = (size_t)cal * S + s;
+  const int* L = lo + r * n_a;
+  int* J = jb + r * (n_a + 1);
+  const int prev = j == 0 ? -1 : L[j - 1];
+  const int cur = j == n_a ? n_a : L[j];
+  if (cur < prev || cur > n_a) {   // not monotone: the push/mix pair runs instead
+    atomicOr(flag, 1);
+    return;
+  }
+  for (int d = prev + 1; d <= cur; ++d) J[d] = j;
+}
+
+template <int SMAX>
+__global__ __launch_bounds__(256) void hist_step_kernel(int S, int n_a, const int* __restrict__ lo,
+                                                        const double* __restrict__ wlo, const int* __restrict__ jb,
+                                                        const double* __restrict__ P,
+                                                        const double* __restrict__ mass,
+                                                        double* __restrict__ mass_out, unsigned long long* dslots,
+                                                        int* last_iter, int iter, double tol) {
+  const int cal = blockIdx.y;
+  if (dslots && iter >= 2) {   // same sticky protocol as hist_mix_kernel
+    if (load_u64_agent(&dslots[cal * kSlots + 3]) != 0ull) return;
+    const double dprev = __longlong_as_double((long long)load_u64_agent(&dslots[cal * kSlots + (iter - 1) % 3]));
+    if (!(dprev >= tol)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) store_u64_agent(&dslots[cal * kSlots + 3], 1ull);
+      return;
+    }
+  }
+  extern __shared__ double Tl[];   // [S][kHistTile], dynamic (S x 2 KB)
+  __shared__ int s_off[SMAX + 1];
+  __shared__ int s_jlo[SMAX];
+  const int tid = threadIdx.x;
+  const int d0 = blockIdx.x * kHistTile;
+  const int d1 = min(d0 + kHistTile, n_a);
+  const size_t rows = (size_t)cal * S;
+  for (int q = tid; q < S * kHistTile; q += blockDim.x) Tl[q] = 0.0;
+  if (tid < S) {
+    const int* J = jb + (rows + tid) * (n_a + 1);
+    const int a = J[d0 > 0 ? d0 - 1 : 0];
+    s_jlo[tid] = a;
+    s_off[tid + 1] = J[d1] - a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    s_off[0] = 0;
+    for (int q = 0; q < S; ++q) s_off[q + 1] += s_off[q];
+  }
+  __syncthreads();
+  const int total = s_off[S];
+  for (int k0 = 0; k0 < total; k0 += kHistUnroll * (int)blockDim.x) {
+    int key[kHistUnroll], ss[kHistUnroll], dd[kHistUnroll];
+    double mj[kHistUnroll], wl[kHistUnroll];
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u) {
+      const int k = k0 + u * (int)blockDim.x + tid;
+      const bool act = k < total;
+      int sl = 0, sh = S - 1;   // s with s_off[s] <= k < s_off[s + 1]
+      while (sl < sh) {
+        const int mid = (sl + sh + 1) >> 1;
+        if (s_off[mid] <= k) sl = mid; else sh = mid - 1;
+      }
+      const size_t o = (rows + sl) * n_a + (act ? s_jlo[sl] + (k - s_off[sl]) : 0);
+      ss[u] = sl;
+      dd[u] = act ? lo[o] : -1;
+      key[u] = act ? sl * (n_a + 1) + dd[u] : -1;
+      mj[u] = act ? mass[o] : 0.0;
+      wl[u] = act ? wlo[o] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u) {
+      const bool act = key[u] >= 0;
+      double vlo = wl[u] * mj[u];
+      double vhi = (1.0 - wl[u]) * mj[u];
+      double* Ts = Tl + ss[u] * kHistTile;
+      const int d = dd[u];
+      if (seg_sum(key[u], act, vlo) && d >= d0) atomicAdd(&Ts[d - d0], vlo);
+      if (seg_sum(key[u], act, vhi) && d + 1 < d1) atomicAdd(&Ts[d + 1 - d0], vhi);
+    }
+  }
+  __syncthreads();
+  const int j = d0 + tid;
+  const bool active = j < d1;
+  const size_t base = rows * n_a;
+  double t[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) t[s] = (s < S) ? Tl[s * kHistTile + tid] : 0.0;
+  const double* Pc = P + (size_t)cal * S * S;
+  double dmax = 0.0;
+  for (int sp = 0; sp < S; ++sp) {
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s)
+      if (s < S) acc += Pc[(size_t)s * S + sp] * t[s];
+    if (active) {
+      const size_t o = base + (size_t)sp * n_a + j;
+      dmax = nan_max(dmax, fabs(acc - mass[o]));
+      mass_out[o] = acc;
+    }
+  }
+  if (dslots) {
+    __shared__ double red[256 / kWave];
+    dmax = wave_nan_max(dmax);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = dmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double d = red[0];
+      for (int w2 = 1; w2 < (int)(blockDim.x / kWave); ++w2) d = nan_max(d, red[w2]);
+      atomicMax(&dslots[cal * kSlots + iter % 3], (unsigned long long)__double_as_longlong(d));
+      if (blockIdx.x == 0) {
+        store_u64_agent(&dslots[cal * kSlots + (iter + 1) % 3], 0ull);
+        last_iter[cal] = iter;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void hist_K_kernel(int S, int n_a, const double* __restrict__ mass,
                                                      const double* __restrict__ a_grid, double* __restrict__ K) {
   const int cal = blockIdx.x;
@@ -185,10 +323,10 @@ static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
   h->h_hdist = nullptr; h->h_K = nullptr; h->h_hlast = nullptr; h->hist_cap = 0;
   AIY_HIP(h, hipMalloc((void**)&h->d_hdist, sizeof(unsigned long long) * kSlots * n_cal));
   AIY_HIP(h, hipMalloc((void**)&h->d_K, sizeof(double) * n_cal));
-  AIY_HIP(h, hipMalloc((void**)&h->d_hlast, sizeof(int) * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_hlast, sizeof(int) * (n_cal + 1)));   // + monotone flag
   AIY_HIP(h, hipHostMalloc((void**)&h->h_hdist, sizeof(unsigned long long) * kSlots * n_cal, hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_K, sizeof(double) * n_cal, hipHostMallocDefault));
-  AIY_HIP(h, hipHostMalloc((void**)&h->h_hlast, sizeof(int) * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_hlast, sizeof(int) * (n_cal + 1), hipHostMallocDefault));
   h->hist_cap = n_cal;
   return AIY_OK;
 }
@@ -227,9 +365,27 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
   const size_t per = (size_t)n_cal * S * n_a;
   double* T = work;          // [n_cal][S][n_a] push accumulator (kept zero between iterations)
   double* alt = work + per;  // [n_cal][S][n_a] ping-pong partner of `mass`
-  AIY_HIP(h, hipMemsetAsync(T, 0, per * sizeof(double), st));
   AIY_HIP(h, hipMemsetAsync(h->d_hdist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
-  AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * n_cal, st));
+  AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * (n_cal + 1), st));
+  // Fused path: the tile source ranges jb [n_cal][S][n_a + 1] (int) live in T's space.
+  int* jb = reinterpret_cast<int*>(T);
+  const size_t step_lds = (size_t)S * kHistTile * sizeof(double);
+  bool fused = h->hist_fused && step_lds <= 128 * 1024;
+  if (fused) {
+    hipLaunchKernelGGL(hist_range_kernel, dim3((n_a + 1 + 255) / 256, S, n_cal), dim3(256), 0, st, S, n_a, lo, jb,
+                       h->d_hlast + n_cal);
+    AIY_CHECK_LAUNCH(h);
+    AIY_HIP(h, hipMemcpyAsync(h->h_hlast + n_cal, h->d_hlast + n_cal, sizeof(int), hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipStreamSynchronize(st));
+    fused = h->h_hlast[n_cal] == 0;   // every row monotone
+  }
+  if (!fused) AIY_HIP(h, hipMemsetAsync(T, 0, per * sizeof(double), st));
+  auto step_fn = S <= 8 ? (const void*)hist_step_kernel<8>
+                        : S <= 16 ? (const void*)hist_step_kernel<16>
+                                  : S <= 32 ? (const void*)hist_step_kernel<32> : (const void*)hist_step_kernel<64>;
+  if (fused && step_lds > 48 * 1024)
+    AIY_HIP(h, hipFuncSetAttribute(step_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)step_lds));
+  dim3 gstep((n_a + kHistTile - 1) / kHistTile, n_cal);
   dim3 gpush((n_a + 255) / 256, S, n_cal);
   dim3 gmix((n_a + 255) / 256, n_cal);
   int it = 1;
@@ -238,6 +394,12 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
     for (int k = it; k < end; ++k) {
       const double* src = (k & 1) ? mass : alt;   // iteration k reads buffer (k-1)%2, writes k%2
       double* dst = (k & 1) ? alt : mass;
+      if (fused) {
+        void* args[] = {(void*)&S, (void*)&n_a, (void*)&lo, (void*)&wlo, (void*)&jb, (void*)&P, (void*)&src,
+                        (void*)&dst, (void*)&h->d_hdist, (void*)&h->d_hlast, (void*)&k, (void*)&tol};
+        AIY_HIP(h, hipLaunchKernel(step_fn, gstep, dim3(256), args, step_lds, st));
+        continue;
+      }
       hipLaunchKernelGGL(hist_push_kernel, gpush, dim3(256), 0, st, S, n_a, lo, wlo, src, T, h->d_hdist, k, tol);
       if (S <= 8)
         hipLaunchKernelGGL(hist_mix_kernel<8>, gmix, dim3(256), 0, st, S, n_a, P, T, src, dst, h->d_hdist, h->d_hlast, k, tol);

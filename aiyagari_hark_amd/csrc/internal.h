@@ -36,6 +36,7 @@ struct aiy_handle {
   double* d_K = nullptr;
   int* d_hlast = nullptr;
   size_t hist_cap = 0;
+  bool hist_fused = false;           // AIY_OPT_HIST_FUSED
   unsigned long long* h_hdist = nullptr;
   double* h_K = nullptr;
   int* h_hlast = nullptr;

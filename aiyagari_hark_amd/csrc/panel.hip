@@ -374,6 +374,7 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       if (value < 0 || value > 2) return fail(h, AIY_ERR_ARG, "AIY_OPT_RESIDENT_SHAPE must be 0, 1 or 2");
       h->res_shape = (int)value;
       return AIY_OK;
+    case AIY_OPT_HIST_FUSED: h->hist_fused = value != 0; return AIY_OK;
     default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
   }
 }

@@ -239,6 +239,10 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                  a block of periods as ONE persistent launch (agents resident in
                                  LDS, in-kernel exchange of partial sums per period); 0: one launch
                                  per period */
+#define AIY_OPT_HIST_FUSED 4 /* value != 0: aiy_hist_solve runs one fused push+mix launch per iteration
+                              when every lottery row is monotone; 0 (default): the push/mix pair.  The
+                              fused step moves 28 B per point but its borrowing-constraint tile pulls
+                              thousands of sources serially: measured slower at Table II sizes */
 #define AIY_OPT_RESIDENT_SHAPE 3 /* persistent panel workgroup: 0 (default) 512 threads x 8 agents
                                     per lane per pass, quad-cooperative record loads; 1: 1024
                                     threads x 4, quad-cooperative; 2: 512 x 8, per-lane record

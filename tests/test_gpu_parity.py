@@ -500,3 +500,37 @@ def test_rouwenhorst_25_state_histogram(gpu):
     Kw, info = ST.capital_supply(0.02, dict(DiscFac=0.96, CRRA=5.0, CapShare=0.36, DeprFac=0.08), aGrid, lab, P)
     assert int(cycles[0]) == info["cycles"]
     assert abs(K[0] - Kw) / Kw < 1e-9
+
+
+@pytest.mark.parametrize("S_lab,income,n_a,n_cal", [(7, "tauchen", 1000, 3), (25, "rouwenhorst", 700, 2),
+                                                      (7, "tauchen", 5000, 2)])
+def test_hist_fused_step_matches_push_mix(gpu, S_lab, income, n_a, n_cal):
+    """Fused lottery step (hist_step_kernel, AIY_OPT_HIST_FUSED = 1) vs the default
+    push/mix pair: same stationary mass to 1e-13, same iteration counts, and K_s(r)
+    against the oracle's Young histogram (oracle/stationary.py)."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import Calibration, StationaryBatch
+    from oracle import stationary as ST
+    cals = [Calibration(LaborAR=0.9 - 0.3 * i, LaborSD=0.4, CRRA=1.0 + 2 * i, LaborStatesNo=S_lab, income=income)
+            for i in range(n_cal)]
+    aGrid = ST.make_stationary_grid(0.001, 50.0, n_a, 2)
+    h = _lib.handle(gpu.index)
+    r = np.array([0.02 + 0.004 * i for i in range(n_cal)])
+    out = {}
+    try:
+        for fused in (0, 1):
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_FUSED, fused), "opt")
+            b = StationaryBatch(cals, aGrid, device=gpu)
+            K, cycles, iters = b.capital_supply(r, egm_tol=1e-8, hist_tol=1e-12)
+            out[fused] = (K, iters, b.mass.cpu().numpy())
+    finally:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_FUSED, 0), "opt")
+    K0, it0, m0 = out[0]
+    K1, it1, m1 = out[1]
+    assert np.max(np.abs(it0 - it1)) <= 1          # atomics: summation order is not fixed in either path
+    assert np.max(np.abs(m1 - m0)) < 1e-11
+    assert np.max(np.abs(K1 - K0) / K0) < 1e-11
+    for i, c in enumerate(cals):
+        lab, P = ST.income_process(S_lab, c.LaborAR, c.LaborSD, income)
+        Kw, _ = ST.capital_supply(r[i], dict(DiscFac=0.96, CRRA=c.CRRA, CapShare=0.36, DeprFac=0.08), aGrid, lab, P)
+        assert abs(K1[i] - Kw) / Kw < 1e-9
