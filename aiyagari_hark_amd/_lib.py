@@ -101,6 +101,8 @@ SIGNATURES = {
     "aiy_hist_solve": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
                                         ctypes.c_double, ctypes.c_int32, ctypes.c_int32, vp, vp, c_double_p,
                                         c_int32_p, vp]),
+    "aiy_wealth_stats": (ctypes.c_int32, [vp, vp, vp, ctypes.c_int64, c_double_p, ctypes.c_int32, c_double_p,
+                                          c_double_p, vp]),
 }
 
 _lib = None

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libaiyagari.so")
-SOURCES = ["api.hip", "index.hip", "egm.hip", "panel_tab.hip", "panel.hip", "panel_block.hip", "panel_resident.hip", "hist.hip"]
+SOURCES = ["api.hip", "index.hip", "egm.hip", "panel_tab.hip", "panel.hip", "panel_block.hip", "panel_resident.hip", "hist.hip", "stats.hip"]
 HEADERS = ["common.h", "internal.h", "panel_common.h"]
 ARCH = os.environ.get("AIY_OFFLOAD_ARCH", "gfx950")
 

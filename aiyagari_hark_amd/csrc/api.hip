@@ -43,6 +43,7 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->d_hdist) (void)hipFree(h->d_hdist);
   if (h->d_K) (void)hipFree(h->d_K);
   if (h->d_hlast) (void)hipFree(h->d_hlast);
+  if (h->d_stats) (void)hipFree(h->d_stats);
   if (h->h_hdist) (void)hipHostFree(h->h_hdist);
   if (h->h_K) (void)hipHostFree(h->h_K);
   if (h->h_hlast) (void)hipHostFree(h->h_hlast);

@@ -37,6 +37,9 @@ struct aiy_handle {
   int* d_hlast = nullptr;
   size_t hist_cap = 0;
   bool hist_fused = false;           // AIY_OPT_HIST_FUSED
+  // wealth statistics (stats.hip): sort / scan scratch
+  void* d_stats = nullptr;
+  size_t stats_cap = 0;
   unsigned long long* h_hdist = nullptr;
   double* h_K = nullptr;
   int* h_hlast = nullptr;

@@ -276,6 +276,17 @@ int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, con
                        int32_t max_iter, int32_t chunk, double* mass, double* work, double* K_out,
                        int32_t* iters_out, aiy_stream stream);
 
+/* ------------------- wealth-distribution statistics ------------------- */
+
+/* HARK 0.12 get_lorenz_shares(data, weights, percentiles) and get_percentiles(...) of a
+ * DEVICE array (the notebook's sim_wealth, Aiyagari-HARK.py:311-316): n doubles `data`,
+ * optional device `weights` (NULL: unit weights), n_p <= 256 HOST percentiles in (0, 1).
+ * lorenz_out / pctl_out: HOST [n_p] (either may be NULL).  Scratch is handle-owned.
+ * BLOCKING (synchronises `stream`). */
+int32_t aiy_wealth_stats(aiy_handle* h, const double* data, const double* weights, int64_t n,
+                         const double* pctiles, int32_t n_p, double* lorenz_out, double* pctl_out,
+                         aiy_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

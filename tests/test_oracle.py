@@ -180,3 +180,27 @@ def test_ge_short_run_oracle_anchor():
     assert len(log) >= 2
     assert 0.02 < res["r"] < 0.05
     assert res["saving_rate"] == pytest.approx(0.08 * 0.36 / (res["r"] + 0.08), rel=0.05)
+
+
+def test_hark_utils_closed_form():
+    """oracle/hark_utils.py on data 1..N: cum_data[k] = (k+1)(k+2) / (N (N+1))."""
+    from oracle import hark_utils as HU
+    x = np.arange(1.0, 11.0)
+    rng = np.random.RandomState(0)
+    shuffled = rng.permutation(x)
+    assert abs(HU.get_lorenz_shares(shuffled, percentiles=[0.5])[0] - 30.0 / 110.0) < 1e-15
+    assert abs(HU.get_lorenz_shares(shuffled, percentiles=[0.25])[0] - (6 + 0.5 * 6) / 110.0) < 1e-15
+    assert abs(HU.get_percentiles(shuffled, percentiles=[0.5])[0] - 5.0) < 1e-12
+    assert np.isnan(HU.get_percentiles(shuffled, percentiles=[0.05])[0])      # below cum_dist[0] = 0.1
+    w = np.full(10, 2.0)
+    assert abs(HU.get_lorenz_shares(shuffled, weights=w, percentiles=[0.5])[0] - 30.0 / 110.0) < 1e-15
+
+
+@pytest.mark.parametrize("bad", [[0.0, 0.5], [0.5, 1.0], (0.2, 0.5)])
+def test_wealth_stats_argument_checks(bad):
+    """The device mirror rejects what HARK rejects, before touching the GPU."""
+    from aiyagari_hark_amd import stats
+    from oracle import hark_utils as HU
+    for f in (stats.get_lorenz_shares, stats.get_percentiles, HU.get_lorenz_shares, HU.get_percentiles):
+        with pytest.raises(ValueError):
+            f(np.ones(5), percentiles=bad)

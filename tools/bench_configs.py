@@ -7,6 +7,7 @@ configs[1]); one JSON line per config on stdout, progress on stderr.
   panel   configs[3] per-GPU shard: 12 499 998 agents (1e8 / 8, multiple of 7) x 1 000
           periods of the reference panel (Philox shocks) at N_a = 10 000 -- the population
           no longer fits in LDS, so this is the grid engine (one launch per period).
+  stats   wealth statistics (HARK get_lorenz_shares) of a 12.5M-agent shard in HBM.
   stress  configs[4]: rho = 0.9, sigma = 0.4, CRRA in {1, 3, 5}, 25-state Rouwenhorst,
           N_a = 50 000, Young histogram 25 x 50 000 per calibration.
 
@@ -91,6 +92,25 @@ def panel(n_agents, n_a, periods, device):
                 hbm_frac=18.0 * ap / dt / 8e12, K_last=float(p.hist_A[periods - 1].item()), engine=p._engine(_lib_handle()))
 
 
+def wealth_stats(n, device):
+    """Lorenz shares + percentiles of an n-agent wealth vector resident in HBM (the
+    notebook's 15 pctiles), aiy_wealth_stats: device sort + scans + interpolation."""
+    from aiyagari_hark_amd import stats
+    g = torch.Generator(device=device)
+    g.manual_seed(0)
+    a = torch.exp(torch.randn(n, dtype=torch.float64, device=device, generator=g))
+    pct = np.linspace(0.01, 0.999, 15)
+    stats.get_lorenz_shares(a, percentiles=pct)
+    torch.cuda.synchronize()
+    reps = 5
+    t = time.perf_counter()
+    for _ in range(reps):
+        stats.get_lorenz_shares(a, percentiles=pct)
+    dt = (time.perf_counter() - t) / reps
+    return dict(config="wealth statistics (SURVEY §8f rank 1) of one GPU's panel shard", value=n / dt,
+                unit="agents/s", seconds=dt, agents=n, ms_per_call=1e3 * dt)
+
+
 def _lib_handle():
     from aiyagari_hark_amd import _lib
     return _lib.handle(0)
@@ -98,7 +118,7 @@ def _lib_handle():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="*", default=["table2", "panel", "stress"])
+    ap.add_argument("which", nargs="*", default=["table2", "panel", "stress", "stats"])
     ap.add_argument("--n-a", type=int, default=10000)
     ap.add_argument("--stress-n-a", type=int, default=50000)
     ap.add_argument("--agents", type=int, default=12_499_998)
@@ -121,6 +141,8 @@ def main():
             r = table2(args.n_a, dev)
         elif w == "panel":
             r = panel(args.agents, args.n_a, args.periods, dev)
+        elif w == "stats":
+            r = wealth_stats(args.agents, dev)
         elif w == "stress":
             r = stress(args.stress_n_a, dev)
         else:
