@@ -111,8 +111,11 @@ class StationaryBatch:
         self.mass = torch.empty(shp, dtype=F64, device=dev)
         self.work = torch.empty((2,) + shp, dtype=F64, device=dev)
 
-    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000):
-        """K_s(r) for every calibration (r: array [n_cal])."""
+    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000, warm=False):
+        """K_s(r) for every calibration (r: array [n_cal]).  warm=True starts the
+        distribution iteration from the previous call's stationary mass instead of the
+        uniform one (same fixed point, to hist_tol; used between bisection steps, where r
+        moves by half the bracket each step)."""
         n_cal, S = len(self.cals), self.S
         r = np.asarray(r, dtype=np.float64)
         w, _ = firm_prices(r, self.alpha, self.delta)
@@ -130,19 +133,24 @@ class StationaryBatch:
         h.check(h.lib.aiy_hist_lottery(h.h, n_cal, S, self.n_a, _lib.ptr(m), _lib.ptr(c), _lib.ptr(self.d_a),
                                        _lib.ptr(dR), _lib.ptr(dw), _lib.ptr(self.d_lab), _lib.ptr(self.lo),
                                        _lib.ptr(self.wlo), sp), "aiy_hist_lottery")
-        self.mass.fill_(1.0 / (S * self.n_a))
+        if not (warm and getattr(self, "_mass_valid", False)):
+            self.mass.fill_(1.0 / (S * self.n_a))
         K = (ctypes.c_double * n_cal)()
         iters = (ctypes.c_int32 * n_cal)()
         h.check(h.lib.aiy_hist_solve(h.h, n_cal, S, self.n_a, _lib.ptr(self.lo), _lib.ptr(self.wlo),
                                      _lib.ptr(self.d_P), _lib.ptr(self.d_a), float(hist_tol), int(max_hist), 64,
                                      _lib.ptr(self.mass), _lib.ptr(self.work), K, iters, sp), "aiy_hist_solve")
         self.last_tables = (m, c)
+        self._mass_valid = True
         return np.array(K[:]), np.array(cycles), np.array(iters[:])
 
 
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
-                 hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None):
-    """GE bisection on r (E1) for every calibration at once.  Returns StationaryResult."""
+                 hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True):
+    """GE bisection on r (E1) for every calibration at once.  Returns StationaryResult.
+    warm_hist: each bisection step's distribution iteration starts from the previous
+    step's stationary mass (the oracle, oracle/stationary.py, starts from uniform; both
+    converge to the same distribution to hist_tol)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     b = StationaryBatch(cals, aGrid, device=device)
@@ -155,7 +163,7 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     Ks = np.zeros(n)
     while np.any(hi - lo > r_tol) and steps < max_steps:
         mid = 0.5 * (lo + hi)
-        Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol)
+        Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol, warm=warm_hist and steps > 0)
         _, Kd = firm_prices(mid, b.alpha, b.delta)
         up = Ks > Kd
         hi = np.where(up, mid, hi)

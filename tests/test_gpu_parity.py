@@ -534,3 +534,17 @@ def test_hist_fused_step_matches_push_mix(gpu, S_lab, income, n_a, n_cal):
         lab, P = ST.income_process(S_lab, c.LaborAR, c.LaborSD, income)
         Kw, _ = ST.capital_supply(r[i], dict(DiscFac=0.96, CRRA=c.CRRA, CapShare=0.36, DeprFac=0.08), aGrid, lab, P)
         assert abs(K1[i] - Kw) / Kw < 1e-9
+
+
+def test_bisection_warm_histogram_same_equilibrium(gpu):
+    """Warm-started distribution iteration between bisection steps (solve_table2's
+    default) reaches the cold-started equilibrium: r and K/Y within 1e-9, identical
+    bisection path."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0), Calibration(LaborAR=0.3, LaborSD=0.2, CRRA=1.0)]
+    warm = solve_table2(cals, n_a=400, r_tol=1e-7, device=gpu, warm_hist=True)
+    cold = solve_table2(cals, n_a=400, r_tol=1e-7, device=gpu, warm_hist=False)
+    assert warm.bisection_steps == cold.bisection_steps
+    assert np.max(np.abs(warm.r - cold.r)) < 1e-9
+    assert np.max(np.abs(warm.KtoY - cold.KtoY)) < 1e-9
+    assert sum(int(np.max(i)) for i in warm.hist_iters) < sum(int(np.max(i)) for i in cold.hist_iters)
