@@ -7,6 +7,8 @@ configs[1]); one JSON line per config on stdout, progress on stderr.
   panel   configs[3] per-GPU shard: 12 499 998 agents (1e8 / 8, multiple of 7) x 1 000
           periods of the reference panel (Philox shocks) at N_a = 10 000 -- the population
           no longer fits in LDS, so this is the grid engine (one launch per period).
+  table2_ref  configs[2] in the reference algorithm: 24 KS-form economies (notebook grids,
+          350 agents, act_T = 11 000) to their AFunc fixed points in one EconomyBatch.
   stats   wealth statistics (HARK get_lorenz_shares) of a 12.5M-agent shard in HBM.
   stress  configs[4]: rho = 0.9, sigma = 0.4, CRRA in {1, 3, 5}, 25-state Rouwenhorst,
           N_a = 50 000, Young histogram 25 x 50 000 per calibration.
@@ -111,6 +113,30 @@ def wealth_stats(n, device):
                 unit="agents/s", seconds=dt, agents=n, ms_per_call=1e3 * dt)
 
 
+def table2_reference(device, agents=350):
+    """configs[2] in the reference's own algorithm: the 24 Table II cells, each a
+    Krusell-Smith-form economy with the notebook's grids (32-point asset grid, 15 M nodes,
+    350 agents, act_T = 11 000, T_discard = 1 000), solved to its AFunc fixed point by one
+    EconomyBatch (batched EGM + one block-panel launch per GE iteration), Philox shocks."""
+    from aiyagari_hark_amd.sweep import EconomyBatch, build_economies, table2_grid
+    warm = build_economies(table2_grid()[:2], dict(act_T=300, T_discard=100), dict(AgentCount=agents),
+                           device=device)
+    EconomyBatch(warm).solve()
+    torch.cuda.synchronize()
+    econs = build_economies(table2_grid(), {}, dict(AgentCount=agents), device=device)
+    eb = EconomyBatch(econs)
+    t = time.perf_counter()
+    loops = eb.solve()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    res = eb.results()
+    return dict(config="configs[2] Table II in the reference algorithm (KS-form GE per cell, notebook grids)",
+                value=len(econs) / dt, unit="GE solves/s", seconds=dt, n_cal=len(econs), agents=agents,
+                act_T=econs[0].act_T, ge_iterations=list(loops),
+                r_percent=[round(100 * r["r"], 4) for r in res],
+                saving_rate_percent=[round(100 * r["saving_rate"], 4) for r in res])
+
+
 def _lib_handle():
     from aiyagari_hark_amd import _lib
     return _lib.handle(0)
@@ -118,7 +144,7 @@ def _lib_handle():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="*", default=["table2", "panel", "stress", "stats"])
+    ap.add_argument("which", nargs="*", default=["table2", "table2_ref", "panel", "stress", "stats"])
     ap.add_argument("--n-a", type=int, default=10000)
     ap.add_argument("--stress-n-a", type=int, default=50000)
     ap.add_argument("--agents", type=int, default=12_499_998)
@@ -141,6 +167,8 @@ def main():
             r = table2(args.n_a, dev)
         elif w == "panel":
             r = panel(args.agents, args.n_a, args.periods, dev)
+        elif w == "table2_ref":
+            r = table2_reference(dev)
         elif w == "stats":
             r = wealth_stats(args.agents, dev)
         elif w == "stress":
