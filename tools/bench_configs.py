@@ -149,6 +149,7 @@ def main():
     ap.add_argument("--stress-n-a", type=int, default=50000)
     ap.add_argument("--agents", type=int, default=12_499_998)
     ap.add_argument("--periods", type=int, default=1000)
+    ap.add_argument("--hist-fused", type=int, default=-1, help="AIY_OPT_HIST_FUSED (-1: library default)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     import threading
@@ -161,6 +162,9 @@ def main():
     threading.Thread(target=heartbeat, daemon=True).start()
     from aiyagari_hark_amd import _lib
     _lib.load()
+    if args.hist_fused >= 0:
+        h = _lib.handle(0)
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_FUSED, args.hist_fused), "opt")
     for w in args.which:
         log("start", w)
         if w == "table2":
