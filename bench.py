@@ -159,6 +159,36 @@ def egm_kernel_time(agent, n_launch=20):
     return ms.value / n_launch
 
 
+def table2_reference_leg(world, rank, dev, agents=350):
+    """configs[2] in the reference's own algorithm, reported beside the headline: the 24
+    Table II cells (rho x sigma x CRRA) as KS-form economies with the notebook's grids
+    (32-point asset grid, 15 M nodes, 350 agents, act_T = 11 000), split round-robin over
+    the ranks (parallel.split_calibrations; 3 per GPU at 8 GPUs), each rank solving its
+    cells to their AFunc fixed points in one EconomyBatch; no collective in the data path.
+    Value = 24 / (max over ranks of the wall time)."""
+    from aiyagari_hark_amd.parallel import split_calibrations
+    from aiyagari_hark_amd.sweep import EconomyBatch, build_economies, table2_grid
+    cells = table2_grid()
+    mine = split_calibrations(list(enumerate(cells)), world, rank)
+    warm = build_economies(cells[:1], dict(act_T=300, T_discard=100), dict(AgentCount=agents), device=dev)
+    EconomyBatch(warm).solve()
+    econs = [build_economies([c], {}, dict(AgentCount=agents), device=dev, seed0=k)[0] for k, c in mine]
+    barrier(world)
+    t0 = time.perf_counter()
+    loops = EconomyBatch(econs).solve() if econs else []
+    barrier(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    return {"value": len(cells) / el, "unit": "GE solves/s", "seconds": el, "calibrations": len(cells),
+            "per_rank": len(mine), "agents": agents, "act_T": 11000, "ge_iterations_rank0": list(loops),
+            "workload": "configs[2] Table II, reference algorithm: KS-form GE per cell, notebook grids, "
+                        "one EconomyBatch per rank"}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
@@ -217,6 +247,7 @@ def main():
     ap.add_argument("--act-T", type=int, default=ACT_T)
     ap.add_argument("--t-discard", type=int, default=T_DISCARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-table2", action="store_true", help="skip the Table II reference-algorithm leg")
     ap.add_argument("--no-kernel-diag", action="store_true",
                     help="skip the extra timing launches after the timed region (PMC passes)")
     args = ap.parse_args()
@@ -313,6 +344,8 @@ def main():
                            "algorithmic_bytes_per_launch": egm_bytes, "avg_launch_ms": t_egm_ms},
         "cpu_baseline": None,
     }
+    if not args.no_table2:
+        line["table2_reference"] = table2_reference_leg(world, rank, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         os.environ.setdefault("OMP_NUM_THREADS", "1")
         cb = cpu_baseline(n_ge, cyc)

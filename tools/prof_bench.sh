@@ -11,7 +11,7 @@ stage=${2:-trace}
 export TMPDIR=/tmp
 out=gpurun_out/bench_$tag
 mkdir -p $out
-B="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-diag"
+B="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-diag --no-table2"
 case $stage in
   trace)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 $B > $out/trace.log 2>&1 || exit 1
