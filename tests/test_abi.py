@@ -26,7 +26,8 @@ def lib():
 def test_header_lists_expected_entry_points():
     fns = header_functions()
     for must in ("aiy_create", "aiy_destroy", "aiy_egm_step", "aiy_egm_solve", "aiy_sim_periods",
-                 "aiy_hist_lottery", "aiy_hist_solve", "aiy_comm_init", "aiy_allreduce_sum", "aiy_policy_eval"):
+                 "aiy_hist_lottery", "aiy_hist_solve", "aiy_comm_init", "aiy_allreduce_sum", "aiy_policy_eval",
+                 "aiy_wealth_stats"):
         assert must in fns
 
 
@@ -63,6 +64,7 @@ def test_argument_validation_without_gpu(lib):
     d = _lib.EgmDims(1, 28, 15, 32)
     i = _lib.EgmInputs()
     assert lib.aiy_egm_step(None, ctypes.byref(d), ctypes.byref(i), None, None, None, None, None) == -1
+    assert lib.aiy_wealth_stats(None, None, None, 10, None, 1, None, None, None) == -1
     assert lib.aiy_create(0, None) == -1
     assert lib.aiy_comm_unique_id(None) == -1
     assert lib.aiy_destroy(None) == 0
