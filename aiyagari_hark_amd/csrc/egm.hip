@@ -33,6 +33,11 @@
 namespace aiy {
 
 constexpr int kEgmBlock = 256;
+// Minimum waves per SIMD the cycle kernel is compiled for (register budget); tuning builds
+// override it (tools/egm_time.py).
+#ifndef AIY_EGM_WAVES_PER_EU
+#define AIY_EGM_WAVES_PER_EU 6   // measured: 1 (4 by registers) 195, 5: 174, 6: 161 us per cycle
+#endif
 constexpr int kTile = 64;                     // asset nodes per block (one per lane)
 constexpr int kEgmWaves = kEgmBlock / kWave;  // 4
 // Per-calibration convergence words: 3 rotating distance slots x kSub sub-slots (block b
@@ -144,7 +149,7 @@ __device__ __forceinline__ double egm_phase2(const EgmDev& A, const double* __re
 // slot (n+1)%3 for cycle n+1.  Nothing is written after convergence, so slot
 // (last % 3) keeps the final distance for the host.
 template <int SMAX, bool TERMINAL>
-__global__ __launch_bounds__(kEgmBlock) void egm_cycle_kernel(EgmDev A, const double* __restrict__ m_next,
+__global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) void egm_cycle_kernel(EgmDev A, const double* __restrict__ m_next,
                                                               const double* __restrict__ c_next,
                                                               double* __restrict__ m_out,
                                                               double* __restrict__ c_out,
