@@ -117,13 +117,13 @@ def policy_eval(m_tab, c_tab, M_grid, state, m, M=None, stream=None):
     S, n_M, n1 = m_tab.shape
     dev = m_tab.device
     st = torch.as_tensor(np.asarray(state, dtype=np.int32).ravel()).to(dev)
-    mq = torch.as_tensor(np.asarray(m, dtype=np.float64).ravel()).to(dev)
+    mq = torch.from_numpy(np.array(m, dtype=np.float64).ravel()).to(dev)
     n = mq.numel()
     if st.numel() == 1 and n > 1:
         st = st.expand(n).contiguous()
     Mq = None
     if n_M > 1:
-        Mq = torch.as_tensor(np.asarray(M, dtype=np.float64).ravel()).to(dev)
+        Mq = torch.from_numpy(np.array(M, dtype=np.float64).ravel()).to(dev)
         if Mq.numel() == 1 and n > 1:
             Mq = Mq.expand(n).contiguous()
     out = torch.empty(n, dtype=F64, device=dev)

@@ -94,3 +94,37 @@ class DeviceSolution:
         if self._Mg is None:
             self._Mg = self.M_grid.cpu().numpy()
         return self._Mg
+
+    # ---- serialization ------------------------------------------
+    def save(self, path, AFunc=None):
+        """Write the policy tables ([S][n_M][n_a + 1] endogenous m and c, the M grid,
+        CRRA) and, optionally, the aggregate saving rules (AS:1973-2005 ``intercept`` /
+        ``slope`` per aggregate state) to an ``.npz`` file.  Plain arrays only, so
+        ``load`` never unpickles."""
+        arrays = dict(m=self.m_host(), c=self.c_host(), M_grid=self.M_grid_host(),
+                      CRRA=np.float64(self.CRRA), format_version=np.int64(SOLUTION_FORMAT))
+        if AFunc is not None:
+            arrays["afunc"] = np.array([[f.intercept, f.slope] for f in AFunc], dtype=np.float64)
+        np.savez(path, **arrays)
+
+    @classmethod
+    def load(cls, path, device):
+        """Inverse of ``save``: returns ``(solution, afunc)`` with the tables resident on
+        ``device``; ``afunc`` is a [n_states][2] (intercept, slope) array or None."""
+        import torch
+
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["format_version"]) != SOLUTION_FORMAT:
+                raise ValueError(f"{path}: solution format {int(z['format_version'])}, expected {SOLUTION_FORMAT}")
+            m, c, Mg = z["m"], z["c"], z["M_grid"]
+            if m.ndim != 3 or m.shape != c.shape or Mg.shape != (m.shape[1],):
+                raise ValueError(f"{path}: inconsistent table shapes m{m.shape} c{c.shape} M_grid{Mg.shape}")
+            afunc = z["afunc"].copy() if "afunc" in z.files else None
+            crra = float(z["CRRA"])
+        to = dict(dtype=torch.float64, device=device)
+        sol = cls(torch.as_tensor(m, **to).contiguous(), torch.as_tensor(c, **to).contiguous(),
+                  torch.as_tensor(Mg, **to).contiguous(), crra)
+        return sol, afunc
+
+
+SOLUTION_FORMAT = 1

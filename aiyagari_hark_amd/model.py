@@ -183,6 +183,18 @@ class AiyagariType:
     def post_solve(self):
         pass
 
+    def save_solution(self, path):
+        """Policies plus the agent's AFunc to ``.npz``."""
+        self.solution[0].save(path, AFunc=self.AFunc)
+
+    def load_solution(self, path):
+        """Restore ``solution[0]`` (device-resident) and AFunc written by ``save_solution``."""
+        sol, afunc = DeviceSolution.load(path, self.device)
+        self.solution = [sol]
+        if afunc is not None:
+            self.AFunc = [AggregateSavingRule(float(i), float(s)) for i, s in afunc]
+        return self.solution
+
     # ---- simulation side ---------------------------------------------------------------
     def reset(self):                          # AS:1158
         self.initialize_sim()

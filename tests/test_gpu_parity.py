@@ -323,6 +323,19 @@ def test_ge_fixed_point_matches_oracle(gpu):
     # cFunc interop (Aiyagari-HARK.py:275)
     xi = agent.solution[0].cFunc[0].xInterpolators
     assert len(xi) == 15 and xi[0].x_list.shape == (33,)
+    # .npz save/load: reloaded device tables evaluate identically
+    import tempfile
+    q_m = np.linspace(0.5, 40.0, 257)
+    q_M = np.full(q_m.shape, float(econ.sow_state["Mnow"]))
+    before = agent.solution[0].cFunc[5](q_m, q_M)
+    afunc_before = [(f.intercept, f.slope) for f in agent.AFunc]
+    with tempfile.TemporaryDirectory() as d:
+        agent.save_solution(os.path.join(d, "sol.npz"))
+        agent.solution = None
+        agent.load_solution(os.path.join(d, "sol.npz"))
+    assert agent.solution[0].m_tab.is_cuda
+    np.testing.assert_array_equal(agent.solution[0].cFunc[5](q_m, q_M), before)
+    assert [(f.intercept, f.slope) for f in agent.AFunc] == afunc_before
 
 
 def test_search_index_equals_binary_search(gpu):
