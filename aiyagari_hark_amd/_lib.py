@@ -30,6 +30,7 @@ AIY_OPT_USE_GRAPHS = 1
 AIY_OPT_RESIDENT = 2
 AIY_OPT_RESIDENT_SHAPE = 3
 AIY_OPT_HIST_FUSED = 4
+AIY_OPT_RESIDENT_STREAM = 5
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -52,7 +53,8 @@ class Market(ctypes.Structure):
 
 class PanelModel(ctypes.Structure):
     _fields_ = [("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32), ("n_lab", ctypes.c_int32),
-                ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp), ("mrkv_hist", vp)]
+                ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp), ("mrkv_hist", vp),
+                ("act_T", ctypes.c_int32)]
 
 
 class PanelBatch(ctypes.Structure):
@@ -77,6 +79,10 @@ SIGNATURES = {
     "aiy_sim_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]),
+    "aiy_sim_period_local": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.c_int64, ctypes.c_int64, vp, vp,
+                                              vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, vp, vp]),
+    "aiy_sim_period_prices": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market),
+                                               ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
     "aiy_sim_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                              vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), vp]),

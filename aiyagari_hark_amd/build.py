@@ -1,8 +1,8 @@
 """Build libaiyagari.so (hand-written HIP for gfx950) in-tree.
 
-``python -m aiyagari_hark_amd.build`` compiles ``csrc/*.hip`` with hipcc into
-``aiyagari_hark_amd/lib/libaiyagari.so``.  The shared object is git-ignored but
-travels with the repo snapshot to the GPU box.
+``python -m aiyagari_hark_amd.build`` compiles ``csrc/*.hip`` with hipcc (one object per
+translation unit, in parallel) and links ``aiyagari_hark_amd/lib/libaiyagari.so``.  The
+shared object is git-ignored but travels with the repo snapshot to the GPU box.
 """
 from __future__ import annotations
 
@@ -10,14 +10,18 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libaiyagari.so")
-SOURCES = ["api.hip", "index.hip", "egm.hip", "panel_tab.hip", "panel.hip", "panel_block.hip", "panel_resident.hip", "hist.hip", "stats.hip"]
+SOURCES = ["api.hip", "index.hip", "egm.hip", "panel_tab.hip", "panel.hip", "panel_block.hip", "panel_resident.hip",
+           "hist.hip", "hist_resident.hip", "stats.hip", "ge.hip"]
 HEADERS = ["common.h", "internal.h", "panel_common.h"]
 ARCH = os.environ.get("AIY_OFFLOAD_ARCH", "gfx950")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
+          "-I/opt/rocm/include"]
 
 
 def hipcc() -> str:
@@ -27,11 +31,15 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found; the MI355X build needs ROCm's hipcc")
 
 
+def sources():
+    return [f for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
+
+
 def needs_rebuild() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps = [os.path.join(CSRC, f) for f in sources() + HEADERS]
     deps.append(os.path.join(HERE, "..", "include", "aiyagari.h"))
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
@@ -40,17 +48,29 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     if out == LIB and not force and not needs_rebuild():
         return LIB
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    cc = hipcc()
+    flags = [f"--offload-arch={ARCH}"] + CFLAGS + [f"-D{d}" for d in defines]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [cc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print("[aiyagari build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = min(len(sources()), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources()))
     tmp = out + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
-           "-I/opt/rocm/include"]
-    cmd += [f"-D{d}" for d in defines]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
-    cmd += ["-L/opt/rocm/lib", "-lrccl", "-o", tmp]
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-L/opt/rocm/lib", "-lrccl", "-o", tmp]
     if verbose:
         print("[aiyagari build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    shutil.rmtree(objdir, ignore_errors=True)
     return out
 
 

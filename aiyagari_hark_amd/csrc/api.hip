@@ -4,7 +4,7 @@
 #include <cstring>
 #include <new>
 
-extern "C" int32_t aiy_version(void) { return 100; }  // 0.1.0
+extern "C" int32_t aiy_version(void) { return 200; }  // 0.2.0
 
 extern "C" int32_t aiy_create(int32_t device, aiy_handle** out) {
   if (!out) return AIY_ERR_ARG;
@@ -47,6 +47,7 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->h_hdist) (void)hipHostFree(h->h_hdist);
   if (h->h_K) (void)hipHostFree(h->h_K);
   if (h->h_hlast) (void)hipHostFree(h->h_hlast);
+  if (h->hand_ev) (void)hipEventDestroy(h->hand_ev);
   delete h;
   return AIY_OK;
 }

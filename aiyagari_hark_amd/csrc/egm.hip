@@ -329,6 +329,7 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
   AIY_HIP(h, hipSetDevice(h->device));
   EgmDev A = to_dev(dims, in);
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   const long long rows = (long long)dims->n_cal * dims->S * dims->n_M;
   const int* ix = nullptr;
   if (m_next) {
@@ -355,6 +356,7 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   rc = ensure_egm_scratch(h, dims->n_cal);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   const int n_cal = dims->n_cal;
   const size_t per_cal = (size_t)dims->S * dims->n_M * (dims->n_a + 1);
   const size_t buf = per_cal * n_cal;
@@ -436,6 +438,7 @@ extern "C" int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, 
   AIY_HIP(h, hipSetDevice(h->device));
   EgmDev A = to_dev(dims, in);
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   const long long rows = (long long)dims->n_cal * dims->S * dims->n_M;
   rc = ensure_egm_index(h, (size_t)rows * kIdxRow);
   if (rc) return rc;

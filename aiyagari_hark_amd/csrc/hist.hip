@@ -362,6 +362,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
   int32_t rc = ensure_hist_scratch(h, n_cal);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   const size_t per = (size_t)n_cal * S * n_a;
   double* T = work;          // [n_cal][S][n_a] push accumulator (kept zero between iterations)
   double* alt = work + per;  // [n_cal][S][n_a] ping-pong partner of `mass`

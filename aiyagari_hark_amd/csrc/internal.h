@@ -54,9 +54,14 @@ struct aiy_handle {
   void* d_blk = nullptr;
   void* h_blk = nullptr;
   size_t blk_cap = 0;
+  bool res_stream = false;           // AIY_OPT_RESIDENT_STREAM
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // stream hand-off between calls that share the scratch above (aiy::use_stream)
+  hipStream_t last_stream = nullptr;
+  bool has_last_stream = false;
+  hipEvent_t hand_ev = nullptr;
 };
 
 namespace aiy {
@@ -84,6 +89,28 @@ inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
 #define AIY_CHECK_LAUNCH(h) AIY_HIP(h, hipGetLastError())
 
 inline hipStream_t as_stream(aiy_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Calls that use handle scratch go through here with their stream: when the stream
+// differs from the previous call's, the new stream waits (device-side) for everything
+// already enqueued on the old one, so two streams never interleave on the scratch.
+inline int32_t use_stream(aiy_handle* h, hipStream_t st) {
+  if (h->has_last_stream && h->last_stream != st) {
+    if (!h->hand_ev) AIY_HIP(h, hipEventCreateWithFlags(&h->hand_ev, hipEventDisableTiming));
+    if (hipEventRecord(h->hand_ev, h->last_stream) == hipSuccess) {
+      AIY_HIP(h, hipStreamWaitEvent(st, h->hand_ev, 0));
+    } else {
+      (void)hipGetLastError();   // the old stream is gone: nothing left to order against
+    }
+  }
+  h->last_stream = st;
+  h->has_last_stream = true;
+  return AIY_OK;
+}
+#define AIY_USE_STREAM(h, st)                        \
+  do {                                               \
+    int32_t _r = aiy::use_stream((h), (st));         \
+    if (_r) return _r;                               \
+  } while (0)
 
 // Measurement hooks: n launches, each bracketed by its own pair of HIP events on `st`,
 // *ms = sum of the per-launch elapsed times (so inter-launch gaps are not charged to

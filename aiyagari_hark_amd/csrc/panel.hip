@@ -267,7 +267,8 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   if (n_local < 0 || n_total < 1 || agent_offset < 0) return fail(h, AIY_ERR_ARG, "bad agent counts");
   if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
   if (u && u_ld < n_local) return fail(h, AIY_ERR_ARG, "u_ld < n_local");
-  if (t0 < 0 || n_periods < 0 || t0 + (int64_t)n_periods > (1 << 20)) return fail(h, AIY_ERR_ARG, "bad period range");
+  if (t0 < 0 || n_periods < 0 || t0 + (int64_t)n_periods > P.act_T)
+    return fail(h, AIY_ERR_ARG, "bad period range [%d, %lld) for act_T=%d", t0, (long long)t0 + n_periods, P.act_T);
   if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
   if (!h->comm && n_local != n_total) return fail(h, AIY_ERR_ARG, "n_local != n_total without a communicator");
   if (n_periods == 0) return AIY_OK;
@@ -275,6 +276,8 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   rc = ensure_panel_scratch(h);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
+  rc = use_stream(h, st);
+  if (rc) return rc;
   const int nb = sim_blocks(n_local);
   PanelRun r;
   r.n = n_local; r.offset = agent_offset; r.n_total = n_total; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld;
@@ -323,6 +326,60 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   return AIY_OK;
 }
 
+// Two-step sharded period (caller-side all-reduce between the steps).
+extern "C" int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* model, int64_t n_local,
+                                        int64_t agent_offset, double* a, uint8_t* lab, const double* u, uint64_t seed,
+                                        uint32_t ge_iter, int32_t t, double* sow, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (!sow) return fail(h, AIY_ERR_ARG, "null sow");
+  PanelDev P;
+  int32_t rc = panel_dev(h, model, P);
+  if (rc) return rc;
+  if (n_local < 0 || agent_offset < 0) return fail(h, AIY_ERR_ARG, "bad agent counts");
+  if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
+  if (t < 0 || t >= P.act_T) return fail(h, AIY_ERR_ARG, "period t=%d outside [0, act_T=%d)", t, P.act_T);
+  if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
+  AIY_HIP(h, hipSetDevice(h->device));
+  rc = ensure_panel_scratch(h);
+  if (rc) return rc;
+  hipStream_t st = as_stream(stream);
+  rc = use_stream(h, st);
+  if (rc) return rc;
+  PanelRun r;
+  r.n = n_local; r.offset = agent_offset; r.n_total = n_local; r.a = a; r.lab = lab; r.u = u; r.u_ld = n_local;
+  r.u_t0 = t; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 0;
+  hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t);
+  if (n_local > 0) {
+    const aiy_market unused{};
+    hipLaunchKernelGGL(sim_period_kernel, dim3(sim_blocks(n_local)), dim3(kSimBlock), 0, st, P, r, unused);
+  } else {
+    hipLaunchKernelGGL(zero_sum_kernel, dim3(1), dim3(64), 0, st, sow);
+  }
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_sim_period_prices(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
+                                         int64_t n_total, int32_t t, double* sow, double* hist_A, double* hist_M,
+                                         aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (!mkt || !sow) return fail(h, AIY_ERR_ARG, "null market/sow");
+  PanelDev P;
+  int32_t rc = panel_dev(h, model, P);
+  if (rc) return rc;
+  if (n_total < 1) return fail(h, AIY_ERR_ARG, "n_total < 1");
+  if (t < 0 || t >= P.act_T) return fail(h, AIY_ERR_ARG, "period t=%d outside [0, act_T=%d)", t, P.act_T);
+  AIY_HIP(h, hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  rc = use_stream(h, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(period_price_kernel, dim3(1), dim3(64), 0, st, *mkt, P.mrkv_hist, (long long)n_total, sow, hist_A,
+                     hist_M);
+  AIY_CHECK_LAUNCH(h);
+  return AIY_OK;
+}
+
 // Timing hook for bench.py: n_launch back-to-back launches of the per-period kernel
 // alone (agent update + block partials + last-block mill) between two HIP events on
 // `stream`; returns the elapsed milliseconds.  Advances the panel state like
@@ -336,10 +393,13 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   PanelDev P;
   int32_t rc = panel_dev(h, model, P);
   if (rc) return rc;
+  if (n_launch > P.act_T) return fail(h, AIY_ERR_ARG, "n_launch=%d > act_T=%d", n_launch, P.act_T);
   AIY_HIP(h, hipSetDevice(h->device));
   rc = ensure_panel_scratch(h);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
+  rc = use_stream(h, st);
+  if (rc) return rc;
   PanelRun r;
   r.n = n_local; r.offset = 0; r.n_total = n_local; r.a = a; r.lab = lab; r.u = nullptr; r.u_ld = 0; r.u_t0 = 0;
   r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
@@ -375,6 +435,7 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       h->res_shape = (int)value;
       return AIY_OK;
     case AIY_OPT_HIST_FUSED: h->hist_fused = value != 0; return AIY_OK;
+    case AIY_OPT_RESIDENT_STREAM: h->res_stream = value != 0; return AIY_OK;
     default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
   }
 }

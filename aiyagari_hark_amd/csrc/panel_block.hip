@@ -207,6 +207,7 @@ extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* m
   if (n_periods == 0) return AIY_OK;
   AIY_HIP(h, hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   // per-calibration constants -> device scratch (stream-ordered copy of a pinned staging buffer)
   const size_t need = (size_t)M.n_cal * (sizeof(aiy_market) + sizeof(unsigned long long));
   if (need > h->blk_cap) {

@@ -297,7 +297,7 @@ __device__ __forceinline__ void m_bracket(const double* __restrict__ Mg, int n_M
 
 // One calibration's panel model on device (aiy_panel_model).
 struct PanelDev {
-  int S, n_M, n_a, n_lab;
+  int S, n_M, n_a, n_lab, act_T;
   const double* M_grid;
   const double* lab_level;
   const double* lab_cdf;

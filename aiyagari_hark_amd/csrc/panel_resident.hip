@@ -371,7 +371,7 @@ static ResGeometry res_geometry(aiy_handle* h, long long n, int n_cells, const R
   G.nb = (int)((n + G.chunk - 1) / G.chunk);
   const size_t hdr = res_hdr_bytes(n_cells);
   const size_t agents = (size_t)G.chunk * (sizeof(double) + 1);
-  G.in_lds = hdr + agents <= kResLdsBudget;
+  G.in_lds = !h->res_stream && hdr + agents <= kResLdsBudget;
   G.lds = G.in_lds ? (hdr + agents + 15) / 16 * 16 : hdr;
   return G;
 }

@@ -132,7 +132,8 @@ int32_t panel_dev(aiy_handle* h, const aiy_panel_model* model, PanelDev& P) {
   if (!model->tables || !model->lab_level || !model->lab_cdf || !model->mrkv_hist)
     return fail(h, AIY_ERR_ARG, "null model array (tables come from aiy_panel_build)");
   if (model->n_M > 1 && !model->M_grid) return fail(h, AIY_ERR_ARG, "null M_grid");
-  P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab;
+  if (model->act_T < 1 || model->act_T > (1 << 20)) return fail(h, AIY_ERR_ARG, "bad act_T=%d", model->act_T);
+  P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab; P.act_T = model->act_T;
   P.M_grid = model->M_grid; P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf;
   P.mrkv_hist = model->mrkv_hist;
   P.tab = panel_tab(model->tables, panel_tab_geom(model->n_lab, model->n_M, model->n_a));

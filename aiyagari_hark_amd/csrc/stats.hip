@@ -120,6 +120,7 @@ extern "C" int32_t aiy_wealth_stats(aiy_handle* h, const double* data, const dou
     if (!(pctiles[i] > 0.0 && pctiles[i] < 1.0)) return fail(h, AIY_ERR_ARG, "percentiles must lie in (0, 1)");
   AIY_HIP(h, hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
   const size_t nb = (size_t)n * sizeof(double);
   int32_t rc;
   // scratch: [sorted][cd] (+ [w_sorted][cw][w sorted x a] with weights) + percentiles/results + rocPRIM temp

@@ -96,21 +96,24 @@ class DeviceSolution:
         return self._Mg
 
     # ---- serialization ------------------------------------------
-    def save(self, path, AFunc=None):
+    def save(self, path, AFunc=None, **meta):
         """Write the policy tables ([S][n_M][n_a + 1] endogenous m and c, the M grid,
         CRRA) and, optionally, the aggregate saving rules (AS:1973-2005 ``intercept`` /
-        ``slope`` per aggregate state) to an ``.npz`` file.  Plain arrays only, so
-        ``load`` never unpickles."""
+        ``slope`` per aggregate state) and scalar metadata to an ``.npz`` file.  Plain
+        arrays only, so ``load`` never unpickles."""
         arrays = dict(m=self.m_host(), c=self.c_host(), M_grid=self.M_grid_host(),
                       CRRA=np.float64(self.CRRA), format_version=np.int64(SOLUTION_FORMAT))
         if AFunc is not None:
             arrays["afunc"] = np.array([[f.intercept, f.slope] for f in AFunc], dtype=np.float64)
+        for k, v in meta.items():
+            arrays["meta_" + k] = np.asarray(v)
         np.savez(path, **arrays)
 
     @classmethod
-    def load(cls, path, device):
-        """Inverse of ``save``: returns ``(solution, afunc)`` with the tables resident on
-        ``device``; ``afunc`` is a [n_states][2] (intercept, slope) array or None."""
+    def load(cls, path, device, with_meta=False):
+        """Inverse of ``save``: returns ``(solution, afunc)`` (plus the metadata dict when
+        ``with_meta``) with the tables resident on ``device``; ``afunc`` is a
+        [n_states][2] (intercept, slope) array or None."""
         import torch
 
         with np.load(path, allow_pickle=False) as z:
@@ -121,10 +124,11 @@ class DeviceSolution:
                 raise ValueError(f"{path}: inconsistent table shapes m{m.shape} c{c.shape} M_grid{Mg.shape}")
             afunc = z["afunc"].copy() if "afunc" in z.files else None
             crra = float(z["CRRA"])
+            meta = {k[5:]: z[k].item() for k in z.files if k.startswith("meta_")}
         to = dict(dtype=torch.float64, device=device)
         sol = cls(torch.as_tensor(m, **to).contiguous(), torch.as_tensor(c, **to).contiguous(),
                   torch.as_tensor(Mg, **to).contiguous(), crra)
-        return sol, afunc
+        return (sol, afunc, meta) if with_meta else (sol, afunc)
 
 
 SOLUTION_FORMAT = 1

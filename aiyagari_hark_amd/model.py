@@ -183,16 +183,35 @@ class AiyagariType:
     def post_solve(self):
         pass
 
-    def save_solution(self, path):
-        """Policies plus the agent's AFunc to ``.npz``."""
-        self.solution[0].save(path, AFunc=self.AFunc)
+    def save_solution(self, path, economy=None):
+        """Policies plus the agent's AFunc to ``.npz``.  With
+        ``economy`` the file also records how many GE iterations it has completed, so a
+        later ``load_solution(path, economy=...)`` can resume ``economy.solve()``."""
+        extra = {}
+        if economy is not None:
+            extra["ge_iterations"] = np.int64(getattr(economy, "ge_iterations_done", 0))
+        self.solution[0].save(path, AFunc=self.AFunc, **extra)
 
-    def load_solution(self, path):
-        """Restore ``solution[0]`` (device-resident) and AFunc written by ``save_solution``."""
-        sol, afunc = DeviceSolution.load(path, self.device)
+    def load_solution(self, path, economy=None):
+        """Restore ``solution[0]`` (device-resident) and AFunc written by ``save_solution``.
+
+        With ``economy`` the saved saving rules also become the economy's state, so that
+        ``economy.solve()`` resumes the fixed point instead of mixing two rules: its AFunc
+        and the damping state ``intercept_prev`` / ``slope_prev`` that calc_AFunc damps
+        against (AS:1950-1951; updated in place, the reference's aliasing quirk Q9), and
+        the GE iteration count keying the Philox shock counter.  Without ``economy`` the
+        loaded solution is for evaluation (``cFunc``) and for simulation only."""
+        sol, afunc, meta = DeviceSolution.load(path, self.device, with_meta=True)
         self.solution = [sol]
         if afunc is not None:
             self.AFunc = [AggregateSavingRule(float(i), float(s)) for i, s in afunc]
+            if economy is not None:
+                economy.intercept_prev[:] = [float(i) for i, _ in afunc]
+                economy.slope_prev[:] = [float(s) for _, s in afunc]
+                economy.AFunc = [AggregateSavingRule(float(i), float(s)) for i, s in afunc]
+        if economy is not None:
+            economy.ge_iter_base = int(meta.get("ge_iterations", 0))
+            economy.ge_iterations_done = economy.ge_iter_base
         return self.solution
 
     # ---- simulation side ---------------------------------------------------------------
@@ -328,8 +347,9 @@ class AiyagariEconomy:
         loops = 0
         old = None
         self.ge_log = []
+        base = int(getattr(self, "ge_iter_base", 0))   # > 0 when resuming from load_solution
         while go:
-            self._ge_iter = loops
+            self._ge_iter = base + loops                 # keys the Philox shock counter
             self.solve_agents()
             self.make_history()
             new = self.update_dynamics()
@@ -339,6 +359,7 @@ class AiyagariEconomy:
                                     distance=distance, Rnow=self.sow_state["Rnow"]))
             old = new
             loops += 1
+            self.ge_iterations_done = base + loops
             go = distance >= self.tolerance and loops < self.max_loops
         self.dynamics = new
 

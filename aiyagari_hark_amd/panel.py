@@ -77,20 +77,34 @@ class DevicePanel:
         h = _lib.handle(self.device.index)
         keep["tables"] = build_tables(h, m_pol[None], c_pol[None], n_lab, self.device)
         ptrs = [_lib.ptr(keep[k]) for k in ("tables", "M_grid", "lab_level", "lab_cdf", "mrkv_hist")]
-        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *ptrs)
+        # periods a call may simulate: the history buffers and the Mrkv history must cover them
+        self.model_T = min(self.act_T, int(keep["mrkv_hist"].numel()))
+        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *ptrs, self.model_T)
         mk = make_market(market)
         pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *ptrs)
         self._model = (pm, mk, keep, pb)
 
     def run(self, t0: int, n_periods: int, shock_mode="philox", seed=0, ge_iter=0, u_host_source=None,
-            chunk=1000, stream=None):
+            chunk=1000, stream=None, allreduce=None):
         """Simulate periods [t0, t0 + n_periods).  For shock_mode='numpy', u_host_source(n)
-        must return the next n x n_local uniforms (host)."""
+        must return the next n x n_local uniforms (host).
+
+        allreduce: for an agent-sharded panel without a communicator bound in the library
+        (parallel.bind_rccl), a callable that sums the 1-element device tensor it is given
+        over all ranks in place (parallel.torch_allreduce: torch.distributed over RCCL or
+        gloo); each period then runs as aiy_sim_period_local -> allreduce ->
+        aiy_sim_period_prices."""
         if self._model is None:
             raise RuntimeError("bind_model() first")
+        if t0 < 0 or n_periods < 0 or t0 + n_periods > self.model_T:
+            raise ValueError(f"periods [{t0}, {t0 + n_periods}) outside the history [0, {self.model_T})")
         pm, mk, _, pb = self._model
         h = _lib.handle(self.device.index)
         sp = _lib.stream_ptr(stream)
+        if allreduce is not None:
+            self._run_stepwise(h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
+                               allreduce)
+            return
         if self._engine(h) == "block":
             if self.n_total != self.n_local or self.agent_offset != 0:
                 raise ValueError("the block engine does not shard agents")
@@ -121,6 +135,37 @@ class DevicePanel:
                                           _lib.ptr(self.hist_A), _lib.ptr(self.hist_M), sp), "aiy_sim_periods")
             torch.cuda.current_stream(self.device).synchronize() if stream is None else stream.synchronize()
             del ud
+            t += n
+
+    def _run_stepwise(self, h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
+                      allreduce):
+        """Sharded periods with the all-reduce done by the caller between the library's two
+        steps (Aiyagari_Support.py:1868, np.mean over all ranks' agents)."""
+        if shock_mode not in ("philox", "numpy"):
+            raise ValueError(shock_mode)
+        red = self.sow[6:7]
+        t, end = t0, t0 + n_periods
+        while t < end:
+            n = min(chunk, end - t)
+            ud = None
+            if shock_mode == "numpy":
+                u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
+                if u.shape != (n, self.n_local):
+                    raise ValueError(f"u block shape {u.shape} != {(n, self.n_local)}")
+                ud = torch.from_numpy(u).to(self.device)
+            for k in range(n):
+                up = None if ud is None else ud[k].data_ptr()
+                h.check(h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), self.n_local, self.agent_offset,
+                                                   _lib.ptr(self.a), _lib.ptr(self.lab), up,
+                                                   int(seed) & ((1 << 64) - 1), int(ge_iter), int(t + k),
+                                                   _lib.ptr(self.sow), sp), "aiy_sim_period_local")
+                allreduce(red)
+                h.check(h.lib.aiy_sim_period_prices(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_total, int(t + k),
+                                                    _lib.ptr(self.sow), _lib.ptr(self.hist_A), _lib.ptr(self.hist_M),
+                                                    sp), "aiy_sim_period_prices")
+            if ud is not None:
+                torch.cuda.current_stream(self.device).synchronize()
+                del ud
             t += n
 
     def sow_host(self):
@@ -167,7 +212,7 @@ def run_block(h, pb, markets_ref, n_agents, a, lab, seeds, ge_iter, t0, n_period
         n = min(chunk, end - t)
         u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
         want = (pb.n_cal, n, n_agents)
-        if u.size != np.prod(want):
+        if u.shape != want and not (pb.n_cal == 1 and u.shape == want[1:]):
             raise ValueError(f"u block shape {u.shape} != {want}")
         ud = torch.from_numpy(u.reshape(want)).to(a.device)
         h.check(h.lib.aiy_sim_block_periods(h.h, ctypes.byref(pb), markets_ref, n_agents, _lib.ptr(a), _lib.ptr(lab),

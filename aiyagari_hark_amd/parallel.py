@@ -59,7 +59,9 @@ def bind_rccl(handle: "_lib.Handle", group=None):
         if rc != _lib.AIY_OK:
             raise _lib.AiyagariLibError("aiy_comm_unique_id failed")
     obj = [bytes(buf.raw) if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0, group=group)
+    # src is a GLOBAL rank: the group's rank 0 (a subgroup need not contain global rank 0)
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(obj, src=src, group=group)
     uid = ctypes.create_string_buffer(obj[0], 128)
     handle.check(handle.lib.aiy_comm_init(handle.h, uid, world, rank), "aiy_comm_init")
     return world, rank
@@ -67,3 +69,24 @@ def bind_rccl(handle: "_lib.Handle", group=None):
 
 def unbind_rccl(handle: "_lib.Handle"):
     handle.check(handle.lib.aiy_comm_destroy(handle.h), "aiy_comm_destroy")
+
+
+def torch_allreduce(group=None):
+    """Caller-side all-reduce for DevicePanel.run(allreduce=...): sums a small device
+    tensor over ``group`` in place.  With the nccl backend (RCCL on ROCm) the collective
+    runs on the device tensor, ordered on the current stream; with gloo the value makes a
+    round trip through the host (tests and CPU-rendezvous runs)."""
+    import torch.distributed as dist
+
+    backend = dist.get_backend(group)
+
+    def reduce(t):
+        if backend == "gloo":
+            h = t.detach().to("cpu")
+            dist.all_reduce(h, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=group)
+
+    reduce.backend = backend
+    return reduce

@@ -16,6 +16,11 @@
  *  - `stream` is a hipStream_t (NULL = the default stream).  Calls that only enqueue
  *    work are asynchronous; calls documented as BLOCKING synchronise `stream`.
  *  - One handle per (process, device); a handle is not re-entrant across threads.
+ *  - Streams: calls that use the handle's scratch (EGM convergence slots and search
+ *    index, panel partial sums, histogram slots, statistics scratch) may be given any
+ *    stream; when a call arrives on a different stream than the previous one, the
+ *    library makes the new stream wait for the old one (event hand-off), so work on two
+ *    streams through one handle is serialised, never interleaved on the scratch.
  *
  * Table layout for consumption policies (the (x_list, y_list) of the reference's
  * 28 x 15 LinearInterp objects, AS:1509-1516):
@@ -139,8 +144,9 @@ typedef struct {
   const double* M_grid;     /* [n_M]                                                       */
   const double* lab_level;  /* [n_lab] LSStates (AS:1265)                                  */
   const double* lab_cdf;    /* [n_lab][n_lab] cumsum(P[l]) / last (np.random.choice)        */
-  const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805); must cover every period
-                               a call simulates (t0 + n_periods <= act_T)                    */
+  const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805)                          */
+  int32_t act_T;            /* length of mrkv_hist and of the hist_A / hist_M buffers: every
+                               call is checked to simulate periods t0 + n_periods <= act_T   */
 } aiy_panel_model;
 
 /* Panel policy tables (get_controls, AS:1326-1408).  Each period an agent of labour
@@ -175,7 +181,8 @@ int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, in
  *      with np.random.choice)
  *   agent_offset: global index of local agent 0 (Philox counter, sharding)
  * With a communicator bound (aiy_comm_init) the per-period sum of a is all-reduced
- * over RCCL before the prices are formed; otherwise n_local must equal n_total.
+ * over RCCL before the prices are formed; otherwise n_local must equal n_total (or use
+ * the two-step form below with a caller-side all-reduce).
  * Asynchronous, except that the persistent path (AIY_OPT_RESIDENT) and hipGraph replay
  * (single rank, n_periods >= 128) return after the periods completed. */
 int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
@@ -183,6 +190,24 @@ int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_m
                         uint8_t* lab, const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter,
                         int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
                         aiy_stream stream);
+
+/* One sharded period in two steps with the all-reduce left to the caller (any backend:
+ * torch.distributed over RCCL or gloo, MPI, ...): the agent-sharded form of
+ * np.mean(np.array(aNow)) (AS:1868).
+ *   aiy_sim_period_local:  period t of the n_local agents (get_shocks .. get_poststates,
+ *                          AS:1217-1415); leaves their sum of a in sow[6] (device).
+ *                          u: NULL (Philox by global index) or n_local host uniforms of
+ *                          period t.
+ *   -- caller: sow[6] <- sum over ranks of sow[6] --
+ *   aiy_sim_period_prices: mill / calc_R_and_W (AS:1839-1894) on sow[6] / n_total; writes
+ *                          sow, hist_A[t], hist_M[t] and advances sow[7] to t + 1.
+ * Both asynchronous on `stream`. */
+int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* model, int64_t n_local,
+                             int64_t agent_offset, double* a, uint8_t* lab, const double* u,
+                             uint64_t seed, uint32_t ge_iter, int32_t t, double* sow, aiy_stream stream);
+int32_t aiy_sim_period_prices(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
+                              int64_t n_total, int32_t t, double* sow, double* hist_A, double* hist_M,
+                              aiy_stream stream);
 
 /* Measurement hook (bench.py): n_launch periods of the panel kernel (single rank,
  * Philox shocks) -- n_launch per-period launches, each bracketed by its own pair of HIP
@@ -247,6 +272,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     per lane per pass, quad-cooperative record loads; 1: 1024
                                     threads x 4, quad-cooperative; 2: 512 x 8, per-lane record
                                     loads (results identical) */
+#define AIY_OPT_RESIDENT_STREAM 5 /* value != 0: the persistent panel streams agents from HBM even
+                                     when the workgroup slice would fit in LDS (the path panels of
+                                     more than ~4M agents take; for tests and measurement) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

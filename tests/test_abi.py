@@ -27,7 +27,7 @@ def test_header_lists_expected_entry_points():
     fns = header_functions()
     for must in ("aiy_create", "aiy_destroy", "aiy_egm_step", "aiy_egm_solve", "aiy_sim_periods",
                  "aiy_hist_lottery", "aiy_hist_solve", "aiy_comm_init", "aiy_allreduce_sum", "aiy_policy_eval",
-                 "aiy_wealth_stats"):
+                 "aiy_wealth_stats", "aiy_sim_period_local", "aiy_sim_period_prices"):
         assert must in fns
 
 
@@ -53,13 +53,13 @@ def test_struct_layouts(lib):
     assert ctypes.sizeof(_lib.EgmDims) == 16
     assert ctypes.sizeof(_lib.EgmInputs) == 9 * 8
     assert ctypes.sizeof(_lib.Market) == 6 * 8
-    assert ctypes.sizeof(_lib.PanelModel) == 16 + 5 * 8
+    assert ctypes.sizeof(_lib.PanelModel) == 16 + 5 * 8 + 8   # + act_T (padded)
     assert ctypes.sizeof(_lib.PanelBatch) == 24 + 5 * 8
 
 
 def test_argument_validation_without_gpu(lib):
     from aiyagari_hark_amd import _lib
-    assert lib.aiy_version() == 100
+    assert lib.aiy_version() == 200
     # null handle -> AIY_ERR_ARG, nothing launched
     d = _lib.EgmDims(1, 28, 15, 32)
     i = _lib.EgmInputs()

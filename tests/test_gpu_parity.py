@@ -561,3 +561,39 @@ def test_bisection_warm_histogram_same_equilibrium(gpu):
     assert np.max(np.abs(warm.r - cold.r)) < 1e-9
     assert np.max(np.abs(warm.KtoY - cold.KtoY)) < 1e-9
     assert sum(int(np.max(i)) for i in warm.hist_iters) < sum(int(np.max(i)) for i in cold.hist_iters)
+
+
+def test_load_solution_resumes_ge_loop(gpu, tmp_path):
+    """save after one GE iteration, load into a FRESH economy + agent with
+    ``economy=``, resume econ.solve(): the resumed iterations reproduce iterations 1..k of
+    the uninterrupted solve (same damping state intercept_prev / slope_prev, same saving
+    rule, same Philox GE-iteration keys), bit for bit."""
+    from aiyagari_hark_amd.model import AiyagariEconomy, AiyagariType
+
+    def pair():
+        econ = AiyagariEconomy(act_T=600, T_discard=200, intercept_prev=[0.0, 0.0], slope_prev=[1.0, 1.0])
+        econ.verbose = False
+        agent = AiyagariType(device=gpu, shock_mode="philox", shock_seed=3, AgentCount=700)
+        agent.cycles = 0
+        agent.get_economy_data(econ)
+        econ.agents = [agent]
+        econ.make_Mrkv_history()
+        return econ, agent
+
+    full, _ = pair()
+    full.max_loops = 3
+    full.solve()
+    first, agent1 = pair()
+    first.max_loops = 1
+    first.solve()
+    path = str(tmp_path / "ge1.npz")
+    agent1.save_solution(path, economy=first)
+    econ2, agent2 = pair()
+    agent2.load_solution(path, economy=econ2)
+    assert econ2.intercept_prev == first.intercept_prev and econ2.slope_prev == first.slope_prev
+    econ2.max_loops = 2
+    econ2.solve()
+    for a, b in zip(econ2.ge_log, full.ge_log[1:]):
+        assert a["intercept"] == b["intercept"] and a["slope"] == b["slope"]
+        assert a["cycles"] == b["cycles"]
+    assert econ2.sow_state["Rnow"] == full.sow_state["Rnow"]
