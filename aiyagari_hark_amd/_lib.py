@@ -31,6 +31,8 @@ AIY_OPT_RESIDENT = 2
 AIY_OPT_RESIDENT_SHAPE = 3
 AIY_OPT_HIST_FUSED = 4
 AIY_OPT_RESIDENT_STREAM = 5
+AIY_OPT_HIST_RESIDENT = 6
+AIY_OPT_HIST_CLUSTER = 7
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -72,6 +74,9 @@ SIGNATURES = {
     "aiy_egm_step": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), vp, vp, vp, vp, vp]),
     "aiy_egm_solve": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, c_int32_p, c_double_p, vp]),
+    "aiy_egm_solve_from": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), ctypes.c_double,
+                                            ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp, c_int32_p,
+                                            c_double_p, vp]),
     "aiy_egm_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(EgmDims), ctypes.POINTER(EgmInputs), vp, vp, vp, vp,
                                              ctypes.c_int32, ctypes.POINTER(ctypes.c_float), vp]),
     "aiy_policy_eval": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp,
@@ -107,6 +112,7 @@ SIGNATURES = {
     "aiy_hist_solve": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp,
                                         ctypes.c_double, ctypes.c_int32, ctypes.c_int32, vp, vp, c_double_p,
                                         c_int32_p, vp]),
+    "aiy_hist_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
     "aiy_wealth_stats": (ctypes.c_int32, [vp, vp, vp, ctypes.c_int64, c_double_p, ctypes.c_int32, c_double_p,
                                           c_double_p, vp]),
 }

@@ -344,9 +344,10 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
   return AIY_OK;
 }
 
-extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
-                                 int32_t max_cycles, int32_t chunk, double* work_m, double* work_c, double* m_out,
-                                 double* c_out, int32_t* cycles_out, double* dist_out, aiy_stream stream) {
+static int32_t egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                              int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
+                              double* work_m, double* work_c, double* m_out, double* c_out, int32_t* cycles_out,
+                              double* dist_out, aiy_stream stream) {
   int32_t rc = check_egm(h, dims, in);
   if (rc) return rc;
   if (!work_m || !work_c || !m_out || !c_out || !cycles_out || !dist_out) return fail(h, AIY_ERR_ARG, "null buffer");
@@ -367,14 +368,22 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   if (rc) return rc;
   AIY_HIP(h, hipMemsetAsync(h->d_dist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
   AIY_HIP(h, hipMemsetAsync(h->d_last, 0, sizeof(int) * n_cal, st));
+  const bool warm = m_init != nullptr;
+  if (warm) {   // cycle 0 = the caller's tables (ping-pong slot 0) and their search index
+    AIY_HIP(h, hipMemcpyAsync(work_m, m_init, buf * sizeof(double), hipMemcpyDeviceToDevice, st));
+    AIY_HIP(h, hipMemcpyAsync(work_c, c_init, buf * sizeof(double), hipMemcpyDeviceToDevice, st));
+    rc = launch_build_index(h, work_m, rows, dims->n_a + 1, h->d_egm_idx, st);
+    if (rc) return rc;
+  }
   const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
   int next = 1;
   while (true) {
     const int end = std::min(next + chunk, last_allowed + 1);
     for (int cyc = next; cyc < end; ++cyc) {
-      const double* mn = cyc == 1 ? nullptr : work_m + ((cyc - 1) & 1) * buf;
-      const double* cn = cyc == 1 ? nullptr : work_c + ((cyc - 1) & 1) * buf;
-      const int* ix = cyc == 1 ? nullptr : h->d_egm_idx + ((cyc - 1) & 1) * idx_per;
+      const bool term = cyc == 1 && !warm;
+      const double* mn = term ? nullptr : work_m + ((cyc - 1) & 1) * buf;
+      const double* cn = term ? nullptr : work_c + ((cyc - 1) & 1) * buf;
+      const int* ix = term ? nullptr : h->d_egm_idx + ((cyc - 1) & 1) * idx_per;
       launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, ix, cyc, h->d_dist, h->d_last, tol,
                    st);
       rc = launch_build_index(h, work_m + (cyc & 1) * buf, rows, dims->n_a + 1, h->d_egm_idx + (cyc & 1) * idx_per, st);
@@ -407,6 +416,22 @@ extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const 
   }
   AIY_HIP(h, hipStreamSynchronize(st));
   return AIY_OK;
+}
+
+extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                                 int32_t max_cycles, int32_t chunk, double* work_m, double* work_c, double* m_out,
+                                 double* c_out, int32_t* cycles_out, double* dist_out, aiy_stream stream) {
+  return egm_solve_impl(h, dims, in, tol, max_cycles, chunk, nullptr, nullptr, work_m, work_c, m_out, c_out,
+                        cycles_out, dist_out, stream);
+}
+
+extern "C" int32_t aiy_egm_solve_from(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                                      int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
+                                      double* work_m, double* work_c, double* m_out, double* c_out,
+                                      int32_t* cycles_out, double* dist_out, aiy_stream stream) {
+  if (h && (!m_init || !c_init)) return fail(h, AIY_ERR_ARG, "null initial tables");
+  return egm_solve_impl(h, dims, in, tol, max_cycles, chunk, m_init, c_init, work_m, work_c, m_out, c_out,
+                        cycles_out, dist_out, stream);
 }
 
 extern "C" int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_t n_a, const double* m_tab,

@@ -368,6 +368,26 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
   double* alt = work + per;  // [n_cal][S][n_a] ping-pong partner of `mass`
   AIY_HIP(h, hipMemsetAsync(h->d_hdist, 0, sizeof(unsigned long long) * kSlots * n_cal, st));
   AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * (n_cal + 1), st));
+  if (h->hist_resident && !h->hist_fused) {
+    // the whole iteration in one device-resident launch (hist_resident.hip)
+    for (hipEvent_t& e : h->hc_ev)
+      if (!e) AIY_HIP(h, hipEventCreate(&e));
+    rc = hist_solve_resident(h, n_cal, S, n_a, lo, wlo, P, tol, max_iter, mass, h->d_hlast, st);
+    if (rc == AIY_OK) {
+      hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(256), 0, st, S, n_a, mass, a_grid, h->d_K);
+      AIY_CHECK_LAUNCH(h);
+      AIY_HIP(h, hipMemcpyAsync(h->h_hlast, h->d_hlast, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
+      AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
+      AIY_HIP(h, hipStreamSynchronize(st));
+      for (int c = 0; c < n_cal; ++c) {
+        iters_out[c] = h->h_hlast[c];
+        K_out[c] = h->h_K[c];
+      }
+      return AIY_OK;
+    }
+    if (rc != AIY_ERR_UNSUPPORTED) return rc;
+    AIY_HIP(h, hipMemsetAsync(h->d_hlast, 0, sizeof(int) * (n_cal + 1), st));   // push/mix below
+  }
   // Fused path: the tile source ranges jb [n_cal][S][n_a + 1] (int) live in T's space.
   int* jb = reinterpret_cast<int*>(T);
   const size_t step_lds = (size_t)S * kHistTile * sizeof(double);
@@ -440,5 +460,16 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
   AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipStreamSynchronize(st));
   for (int c = 0; c < n_cal; ++c) K_out[c] = h->h_K[c];
+  return AIY_OK;
+}
+
+extern "C" int32_t aiy_hist_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, int32_t reset) {
+  if (!h) return AIY_ERR_ARG;
+  if (ms_sum) *ms_sum = h->hc_ms_sum;
+  if (launches) *launches = h->hc_launches;
+  if (reset) {
+    h->hc_ms_sum = 0.0;
+    h->hc_launches = 0;
+  }
   return AIY_OK;
 }

@@ -37,6 +37,13 @@ struct aiy_handle {
   int* d_hlast = nullptr;
   size_t hist_cap = 0;
   bool hist_fused = false;           // AIY_OPT_HIST_FUSED
+  bool hist_resident = true;         // AIY_OPT_HIST_RESIDENT (hist_resident.hip)
+  int hist_cluster_cap = 0;          // AIY_OPT_HIST_CLUSTER: max workgroups per calibration (0: 32)
+  void* d_hc = nullptr;              // resident histogram: slabs, spans, counters, distances
+  size_t hc_cap = 0;
+  hipEvent_t hc_ev[2] = {nullptr, nullptr};
+  double hc_ms_sum = 0.0;
+  long long hc_launches = 0;
   // wealth statistics (stats.hip): sort / scan scratch
   void* d_stats = nullptr;
   size_t stats_cap = 0;
@@ -67,6 +74,9 @@ struct aiy_handle {
 namespace aiy {
 
 int32_t launch_build_index(aiy_handle* h, const double* x, long long n_rows, int n1, int* H, hipStream_t st);
+int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int* lo, const double* wlo,
+                            const double* P, double tol, int max_iter, double* mass, int* d_iters, hipStream_t st);
+int32_t hist_resident_plan(aiy_handle* h, int n_cal, int S, int n_a, int* out4);
 
 inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
   char buf[512];

@@ -89,8 +89,11 @@ def egm_step(batch: EgmBatch, m_next=None, c_next=None, out=None, stream=None):
     return out
 
 
-def egm_solve(batch: EgmBatch, tol=1e-6, max_cycles=5000, chunk=32, work=None, out=None, stream=None):
+def egm_solve(batch: EgmBatch, tol=1e-6, max_cycles=5000, chunk=32, work=None, out=None, stream=None, init=None):
     """[HARK] solve_agent (infinite horizon, cold start) on device for every calibration.
+    ``init=(m, c)`` warm-starts from those tables instead of the terminal guess
+    (aiy_egm_solve_from; the stationary GE search only -- the KS form keeps HARK's cold
+    start).
 
     Returns (m, c, cycles[n_cal], dist[n_cal])."""
     h = _lib.handle(batch.device.index)
@@ -104,9 +107,18 @@ def egm_solve(batch: EgmBatch, tol=1e-6, max_cycles=5000, chunk=32, work=None, o
     n_cal = shp[0]
     cycles = (ctypes.c_int32 * n_cal)()
     dist = (ctypes.c_double * n_cal)()
-    h.check(h.lib.aiy_egm_solve(h.h, ctypes.byref(d), ctypes.byref(i), float(tol), int(max_cycles), int(chunk),
-                                _lib.ptr(work[0]), _lib.ptr(work[1]), _lib.ptr(out[0]), _lib.ptr(out[1]),
-                                cycles, dist, _lib.stream_ptr(stream)), "aiy_egm_solve")
+    if init is None:
+        h.check(h.lib.aiy_egm_solve(h.h, ctypes.byref(d), ctypes.byref(i), float(tol), int(max_cycles), int(chunk),
+                                    _lib.ptr(work[0]), _lib.ptr(work[1]), _lib.ptr(out[0]), _lib.ptr(out[1]),
+                                    cycles, dist, _lib.stream_ptr(stream)), "aiy_egm_solve")
+    else:
+        m0, c0 = (t.contiguous() for t in init)
+        if tuple(m0.shape) != shp or tuple(c0.shape) != shp:
+            raise ValueError(f"initial table shape {tuple(m0.shape)} != {shp}")
+        h.check(h.lib.aiy_egm_solve_from(h.h, ctypes.byref(d), ctypes.byref(i), float(tol), int(max_cycles),
+                                         int(chunk), _lib.ptr(m0), _lib.ptr(c0), _lib.ptr(work[0]), _lib.ptr(work[1]),
+                                         _lib.ptr(out[0]), _lib.ptr(out[1]), cycles, dist, _lib.stream_ptr(stream)),
+                "aiy_egm_solve_from")
     return out[0], out[1], np.array(cycles[:], dtype=np.int64), np.array(dist[:], dtype=np.float64)
 
 

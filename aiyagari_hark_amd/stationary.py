@@ -2,7 +2,8 @@
 
 ``solve_table2`` solves many calibrations to general equilibrium at once:
 
-  bisection on r (E1)  -- per calibration, all brackets advanced together
+  GE search on r (E1) -- per calibration, all searches advanced together (bisection,
+                          or bisection to a sign change then Brent's method)
     w(r) = (1 - alpha) (alpha / (r + delta))^(alpha / (1 - alpha)),  R = 1 + r
     stationary EGM  -- aiy_egm_solve with one aggregate node (n_M = 1): the reference's
                        solve_Aiyagari arithmetic (Aiyagari_Support.py:1478-1504) with
@@ -111,11 +112,13 @@ class StationaryBatch:
         self.mass = torch.empty(shp, dtype=F64, device=dev)
         self.work = torch.empty((2,) + shp, dtype=F64, device=dev)
 
-    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000, warm=False):
+    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000, warm=False, warm_egm=False):
         """K_s(r) for every calibration (r: array [n_cal]).  warm=True starts the
         distribution iteration from the previous call's stationary mass instead of the
         uniform one (same fixed point, to hist_tol; used between bisection steps, where r
-        moves by half the bracket each step)."""
+        moves by half the bracket each step).  warm_egm=True starts the household solve
+        from the previous call's converged policy (aiy_egm_solve_from): the fixed point
+        moves by ~egm_tol / (1 - beta R), far inside the 1e-5 tolerance on r."""
         n_cal, S = len(self.cals), self.S
         r = np.asarray(r, dtype=np.float64)
         w, _ = firm_prices(r, self.alpha, self.delta)
@@ -125,7 +128,8 @@ class StationaryBatch:
         Wn = torch.as_tensor(np.repeat(w[:, None, None], S, axis=2)).to(dev)
         batch = EgmBatch(self.d_a, torch.zeros((n_cal, 1), dtype=F64, device=dev), self.d_P, Rn, Wn,
                          torch.zeros_like(Rn), self.d_lab, self.d_beta, self.d_crra)
-        m, c, cycles, _ = egm_solve(batch, tol=egm_tol)
+        init = self.last_tables if (warm_egm and getattr(self, "last_tables", None) is not None) else None
+        m, c, cycles, _ = egm_solve(batch, tol=egm_tol, init=init)
         h = _lib.handle(dev.index)
         dR = torch.as_tensor(R).to(dev)
         dw = torch.as_tensor(w).to(dev)
@@ -145,12 +149,96 @@ class StationaryBatch:
         return np.array(K[:]), np.array(cycles), np.array(iters[:])
 
 
+class _Brent:
+    """One calibration's root search on f(r) = K_s(r) - K_d(r) as a coroutine:
+    ``propose()`` gives the next r to evaluate, ``update(f)`` takes f there.
+
+    Until both signs of f have been evaluated it bisects the theoretical bracket
+    [-delta / 2, 1 / beta - 1) (f < 0 below, f > 0 near 1 / beta - 1, where the household
+    solve and the distribution converge slowly, so that endpoint is never evaluated).  It
+    then runs Brent's method on the evaluated bracket (the scipy.optimize.brentq
+    algorithm: secant / inverse quadratic steps, bisection safeguard), stopping within
+    xtol of the root."""
+
+    def __init__(self, lo, hi, xtol):
+        self.lo, self.hi, self.flo, self.fhi, self.xtol = lo, hi, None, None, xtol
+        self.brent = False
+        self.done = False
+        self.x = 0.5 * (lo + hi)
+
+    def propose(self):
+        return self.x
+
+    def update(self, f):
+        if self.done:
+            return
+        if not self.brent:
+            if f > 0:
+                self.hi, self.fhi = self.x, f
+            else:
+                self.lo, self.flo = self.x, f
+            if self.hi - self.lo <= self.xtol:
+                self.done, self.x = True, 0.5 * (self.lo + self.hi)
+                return
+            if self.flo is None or self.fhi is None:
+                self.x = 0.5 * (self.lo + self.hi)
+                return
+            self.brent = True
+            self.xpre, self.fpre, self.xcur, self.fcur = self.lo, self.flo, self.hi, self.fhi
+            self.xblk = self.fblk = self.spre = self.scur = 0.0
+            self._step()
+            return
+        self.xpre, self.fpre = self.xprev_eval, self.fprev_eval
+        self.fcur = f
+        self._step()
+
+    def _step(self):
+        xpre, fpre, xcur, fcur = self.xpre, self.fpre, self.xcur, self.fcur
+        xblk, fblk, spre, scur = self.xblk, self.fblk, self.spre, self.scur
+        if fpre * fcur < 0:
+            xblk, fblk = xpre, fpre
+            spre = scur = xcur - xpre
+        if abs(fblk) < abs(fcur):
+            xpre, xcur, xblk = xcur, xblk, xcur
+            fpre, fcur, fblk = fcur, fblk, fcur
+        delta = 0.5 * (self.xtol + 4 * np.finfo(float).eps * abs(xcur))
+        sbis = 0.5 * (xblk - xcur)
+        if fcur == 0 or abs(sbis) < delta:
+            self.done, self.x = True, xcur
+            return
+        if abs(spre) > delta and abs(fcur) < abs(fpre):
+            if xpre == xblk:
+                stry = -fcur * (xcur - xpre) / (fcur - fpre)
+            else:
+                dpre = (fpre - fcur) / (xpre - xcur)
+                dblk = (fblk - fcur) / (xblk - xcur)
+                stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre))
+            if 2 * abs(stry) < min(abs(spre), 3 * abs(sbis) - delta):
+                spre, scur = scur, stry
+            else:
+                spre = scur = sbis
+        else:
+            spre = scur = sbis
+        self.xprev_eval, self.fprev_eval = xcur, fcur
+        xcur = xcur + (scur if abs(scur) > delta else (delta if sbis > 0 else -delta))
+        self.xpre, self.fpre, self.xcur, self.fcur = xpre, fpre, xcur, fcur
+        self.xblk, self.fblk, self.spre, self.scur = xblk, fblk, spre, scur
+        self.x = xcur
+
+
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
-                 hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True):
-    """GE bisection on r (E1) for every calibration at once.  Returns StationaryResult.
-    warm_hist: each bisection step's distribution iteration starts from the previous
-    step's stationary mass (the oracle, oracle/stationary.py, starts from uniform; both
-    converge to the same distribution to hist_tol)."""
+                 hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
+                 method="bisect", warm_egm=None):
+    """GE on r (E1) for every calibration at once.  Returns StationaryResult.
+
+    method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
+    ge_bisect, step for step); "brent" -- bisection until both signs are evaluated, then
+    Brent's method per calibration to r_tol (about half the K_s evaluations; the same
+    root to r_tol).
+    warm_hist: each step's distribution iteration starts from the previous step's
+    stationary mass (the oracle, oracle/stationary.py, starts from uniform; both converge
+    to the same distribution to hist_tol).  warm_egm (default: on for "brent"): each
+    step's household solve starts from the previous step's policy."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     b = StationaryBatch(cals, aGrid, device=device)
@@ -158,22 +246,43 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     lo = np.full(n, -0.5 * b.delta) if r_lo is None else np.broadcast_to(np.asarray(r_lo, float), (n,)).copy()
     hi = (1.0 / np.array([c.DiscFac for c in cals]) - 1.0 - 1e-9) if r_hi is None else \
         np.broadcast_to(np.asarray(r_hi, float), (n,)).copy()
+    if warm_egm is None:
+        warm_egm = method == "brent"
     steps = 0
     cyc_log, it_log = [], []
     Ks = np.zeros(n)
-    while np.any(hi - lo > r_tol) and steps < max_steps:
-        mid = 0.5 * (lo + hi)
-        Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol, warm=warm_hist and steps > 0)
-        _, Kd = firm_prices(mid, b.alpha, b.delta)
-        up = Ks > Kd
-        hi = np.where(up, mid, hi)
-        lo = np.where(up, lo, mid)
-        steps += 1
-        cyc_log.append(cycles)
-        it_log.append(iters)
-        if log is not None:
-            log.append(dict(step=steps, r=mid.copy(), Ks=Ks.copy(), Kd=Kd.copy()))
-    r = 0.5 * (lo + hi)
+    if method == "brent":
+        search = [_Brent(lo[k], hi[k], r_tol) for k in range(n)]
+        while not all(sr.done for sr in search) and steps < max_steps:
+            x = np.array([sr.propose() for sr in search])
+            Ks, cycles, iters = b.capital_supply(x, egm_tol=egm_tol, hist_tol=hist_tol, warm=warm_hist and steps > 0,
+                                                 warm_egm=warm_egm and steps > 0)
+            _, Kd = firm_prices(x, b.alpha, b.delta)
+            for k, sr in enumerate(search):
+                sr.update(float(Ks[k] - Kd[k]))
+            steps += 1
+            cyc_log.append(cycles)
+            it_log.append(iters)
+            if log is not None:
+                log.append(dict(step=steps, r=x.copy(), Ks=Ks.copy(), Kd=Kd.copy()))
+        r = np.array([sr.propose() for sr in search])
+    elif method == "bisect":
+        while np.any(hi - lo > r_tol) and steps < max_steps:
+            mid = 0.5 * (lo + hi)
+            Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol,
+                                                 warm=warm_hist and steps > 0, warm_egm=warm_egm and steps > 0)
+            _, Kd = firm_prices(mid, b.alpha, b.delta)
+            up = Ks > Kd
+            hi = np.where(up, mid, hi)
+            lo = np.where(up, lo, mid)
+            steps += 1
+            cyc_log.append(cycles)
+            it_log.append(iters)
+            if log is not None:
+                log.append(dict(step=steps, r=mid.copy(), Ks=Ks.copy(), Kd=Kd.copy()))
+        r = 0.5 * (lo + hi)
+    else:
+        raise ValueError(f"method {method!r}")
     _, K = firm_prices(r, b.alpha, b.delta)
     KtoY = K ** (1.0 - b.alpha)
     return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,

@@ -102,6 +102,15 @@ int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inp
                       double* m_out, double* c_out, int32_t* cycles_out, double* dist_out,
                       aiy_stream stream);
 
+/* The same loop warm-started from caller tables m_init/c_init [n_cal][S][n_M][n_a+1]
+ * instead of the terminal guess (build-defined: the stationary GE search E1 re-solves the
+ * household at a nearby r every step; the KS-form GE keeps HARK's cold start, Q12).
+ * Cycle 1 steps from the given tables.  BLOCKING. */
+int32_t aiy_egm_solve_from(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                           int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
+                           double* work_m, double* work_c, double* m_out, double* c_out, int32_t* cycles_out,
+                           double* dist_out, aiy_stream stream);
+
 /* Measurement hook (bench.py): n_launch launches of the EGM cycle kernel alone from
  * (m_next, c_next) (search index built once, outside the timed region), each bracketed
  * by its own pair of HIP events on `stream`; *ms_out = sum of the per-launch elapsed
@@ -275,6 +284,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 #define AIY_OPT_RESIDENT_STREAM 5 /* value != 0: the persistent panel streams agents from HBM even
                                      when the workgroup slice would fit in LDS (the path panels of
                                      more than ~4M agents take; for tests and measurement) */
+#define AIY_OPT_HIST_RESIDENT 6  /* value != 0 (default): aiy_hist_solve runs the whole distribution
+                                    iteration in ONE device-resident launch (a cluster of workgroups
+                                    per calibration, in-kernel barriers); 0: the push/mix launch pair */
+#define AIY_OPT_HIST_CLUSTER 7   /* maximum workgroups per calibration cluster of the resident
+                                    histogram (0: default 32; the minimum the grid size needs wins) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
@@ -303,6 +317,11 @@ int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, con
                        const double* wlo, const double* P, const double* a_grid, double tol,
                        int32_t max_iter, int32_t chunk, double* mass, double* work, double* K_out,
                        int32_t* iters_out, aiy_stream stream);
+
+/* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
+ * the device-resident distribution-iteration launches since the last reset (HIP events on
+ * their stream) and their number.  reset != 0 zeroes the counters.  Host-only. */
+int32_t aiy_hist_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, int32_t reset);
 
 /* ------------------- wealth-distribution statistics ------------------- */
 

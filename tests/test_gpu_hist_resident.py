@@ -1,0 +1,99 @@
+"""GPU tests of the device-resident Young-histogram iteration (csrc/hist_resident.hip,
+build-defined row E2): one launch per aiy_hist_solve, a cluster of workgroups per
+calibration, against the push/mix launch pair (AIY_OPT_HIST_RESIDENT = 0) and the CPU
+oracle (oracle/stationary.py stationary_hist: mass' = P^T lottery_push(mass), stop at the
+first iteration with max |mass' - mass| < tol).
+
+Both device paths sum the lottery contributions with atomics (LDS or global), so their
+masses agree to rounding (1e-13 absolute on masses of order 1e-5), the iteration counts
+to +-1 (a sup-norm change within rounding of the tolerance), and K_s(r) to 1e-12."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(gpu, cals, aGrid, r, resident, cluster=0):
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import StationaryBatch
+    h = _lib.handle(gpu.index)
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_RESIDENT, int(resident)), "opt")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, int(cluster)), "opt")
+    try:
+        b = StationaryBatch(cals, aGrid, device=gpu)
+        K, cycles, iters = b.capital_supply(r, egm_tol=1e-8, hist_tol=1e-12)
+        return K, iters, b.mass.cpu().numpy(), b
+    finally:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_RESIDENT, 1), "opt")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, 0), "opt")
+
+
+def _launches(gpu, reset=True):
+    import ctypes
+    from aiyagari_hark_amd import _lib
+    h = _lib.handle(gpu.index)
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    h.check(h.lib.aiy_hist_launch_stats(h.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "stats")
+    return n.value
+
+
+@pytest.mark.parametrize("shape", ["table2", "mixed", "rouwenhorst", "small_cluster", "tiny"])
+def test_resident_histogram_equals_push_mix(gpu, shape):
+    from aiyagari_hark_amd.stationary import Calibration, table2_calibrations
+    from oracle import stationary as ST
+    cluster = 0
+    if shape == "table2":        # configs[2]: 24 calibrations x 7 states x 10 000 nodes, ONE launch
+        cals, n_a = table2_calibrations(), 10000
+    elif shape == "mixed":
+        cals, n_a = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0), Calibration(LaborAR=0.0, LaborSD=0.2)], 3001
+    elif shape == "rouwenhorst":  # S = 25 (stress shape, smaller grid)
+        cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0, LaborStatesNo=25, income="rouwenhorst")]
+        n_a = 2000
+    elif shape == "small_cluster":   # 3 calibrations per GPU (Table II split over 8 GPUs), cluster of 4
+        cals, n_a, cluster = table2_calibrations()[:3], 10000, 4
+    else:
+        cals, n_a = [Calibration(LaborAR=0.3, LaborSD=0.2, CRRA=3.0)], 40
+    aGrid = ST.make_stationary_grid(0.001, 50.0, n_a, 2)
+    r = np.linspace(0.02, 0.04, len(cals))
+    _launches(gpu)
+    K1, it1, m1, _ = _solve(gpu, cals, aGrid, r, True, cluster)
+    assert _launches(gpu) >= 1, "the resident path did not run"
+    K0, it0, m0, _ = _solve(gpu, cals, aGrid, r, False)
+    assert np.max(np.abs(it1 - it0)) <= 1, (it1, it0)
+    assert np.max(np.abs(m1 - m0)) < 1e-13
+    assert np.max(np.abs(K1 - K0) / K0) < 1e-12
+    assert np.all(np.abs(m1.reshape(len(cals), -1).sum(axis=1) - 1.0) < 1e-10)   # drift over ~1e4 iterations
+
+
+def test_resident_histogram_matches_oracle(gpu):
+    """Against the CPU oracle's lottery + distribution iteration on the same policy."""
+    from aiyagari_hark_amd.stationary import Calibration
+    from oracle import stationary as ST
+    cal = Calibration(LaborAR=0.6, LaborSD=0.4, CRRA=3.0)
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 1500, 2)
+    r = np.array([0.03])
+    K, it, m, b = _solve(gpu, [cal], aGrid, r, True)
+    lab, P = ST.income_process(7, cal.LaborAR, cal.LaborSD, "tauchen")
+    w, _ = ST.prices(0.03, 0.36, 0.08)
+    mt, ct = (x[0].cpu().numpy() for x in b.last_tables)
+    lo, wlo, _ = ST.savings_lottery(mt[:, 0], ct[:, 0], aGrid, 1.03, w, lab)
+    mass, iters, _ = ST.stationary_hist(lo, wlo, P, aGrid.size, tol=1e-12)
+    assert abs(int(it[0]) - iters) <= 1
+    assert np.max(np.abs(m[0] - mass)) < 1e-13
+    Kw = float(np.sum(mass * aGrid[None, :]))
+    assert abs(K[0] - Kw) / Kw < 1e-12
+
+
+def test_resident_histogram_falls_back_when_spans_do_not_fit(gpu):
+    """A cluster so large that the borrowing-constrained columns are covered by more than
+    kHcCand workgroups' spans: the resident launch refuses the shape before iterating and
+    the push/mix pair produces the answer (same as forcing push/mix)."""
+    from aiyagari_hark_amd.stationary import Calibration
+    from oracle import stationary as ST
+    cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=1.0)]
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 2000, 2)
+    r = np.array([0.035])
+    K1, it1, m1, _ = _solve(gpu, cals, aGrid, r, True, cluster=128)
+    K0, it0, m0, _ = _solve(gpu, cals, aGrid, r, False)
+    assert np.max(np.abs(m1 - m0)) < 1e-13
+    assert abs(K1[0] - K0[0]) / K0[0] < 1e-12

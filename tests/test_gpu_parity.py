@@ -597,3 +597,22 @@ def test_load_solution_resumes_ge_loop(gpu, tmp_path):
         assert a["intercept"] == b["intercept"] and a["slope"] == b["slope"]
         assert a["cycles"] == b["cycles"]
     assert econ2.sow_state["Rnow"] == full.sow_state["Rnow"]
+
+
+def test_stationary_brent_warm_matches_oracle_bisection(gpu):
+    """E1 with Brent's method and warm-started household + distribution solves (the bench's
+    Table II settings) lands on the oracle's bisection root: r within 2e-7, K/Y within 1e-5,
+    in fewer K_s evaluations."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    from oracle import stationary as ST
+    cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0),
+            Calibration(LaborAR=0.0, LaborSD=0.4, CRRA=3.0)]
+    res = solve_table2(cals, n_a=150, r_tol=1e-8, device=gpu, method="brent")
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 150, 2)
+    for k, cal in enumerate(cals):
+        lab, P = ST.income_process(7, cal.LaborAR, cal.LaborSD, "tauchen")
+        want = ST.ge_bisect(dict(DiscFac=0.96, CRRA=cal.CRRA, CapShare=0.36, DeprFac=0.08), aGrid, lab, P,
+                            r_tol=1e-8)
+        assert abs(res.r[k] - want["r"]) < 2e-7, (k, res.r[k], want["r"])
+        assert abs(res.KtoY[k] - want["KtoY"]) < 1e-5
+    assert res.bisection_steps < want["iters"]

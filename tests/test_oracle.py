@@ -204,3 +204,39 @@ def test_wealth_stats_argument_checks(bad):
     for f in (stats.get_lorenz_shares, stats.get_percentiles, HU.get_lorenz_shares, HU.get_percentiles):
         with pytest.raises(ValueError):
             f(np.ones(5), percentiles=bad)
+
+
+def test_brent_search_matches_scipy_brentq():
+    """Host logic of the E1 root search (aiyagari_hark_amd.stationary._Brent): bisection
+    until both signs are evaluated, then Brent's method -- the root scipy.optimize.brentq
+    finds, to xtol, on monotone excess-demand-like functions."""
+    from scipy.optimize import brentq
+    from aiyagari_hark_amd.stationary import _Brent
+    funcs = [lambda x: np.exp(40 * (x - 0.035)) - 1.0 - 3.0 * (0.03 - x),
+             lambda x: (x - 0.0123) * (1.0 + 50 * x * x),
+             lambda x: np.tanh(200 * (x + 0.01)) + 0.1 * x]
+    for f in funcs:
+        s = _Brent(-0.04, 0.0416, 1e-10)
+        n = 0
+        while not s.done and n < 100:
+            s.update(f(s.propose()))
+            n += 1
+        want = brentq(f, -0.04, 0.0416, xtol=1e-12)
+        assert abs(s.propose() - want) < 1e-9
+        assert n < 40
+
+
+def test_fast_hist_step_equals_reference_step():
+    """The vectorised CPU bound (np.bincount) equals the np.add.at restatement."""
+    from oracle import stationary as ST
+    rng = np.random.default_rng(1)
+    S, nA = 5, 300
+    lo = np.sort(rng.integers(0, nA - 1, (S, nA)), axis=1)
+    wlo = rng.random((S, nA))
+    mass = rng.random((S, nA))
+    mass /= mass.sum()
+    P = rng.random((S, S))
+    P /= P.sum(axis=1, keepdims=True)
+    a = ST.hist_step(mass, lo, wlo, P)
+    b = ST.hist_step_fast(mass, lo, wlo, P)
+    assert np.max(np.abs(a - b)) < 1e-16
