@@ -33,6 +33,7 @@ AIY_OPT_HIST_FUSED = 4
 AIY_OPT_RESIDENT_STREAM = 5
 AIY_OPT_HIST_RESIDENT = 6
 AIY_OPT_HIST_CLUSTER = 7
+AIY_OPT_HIST_ACCEL = 8
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -65,6 +66,18 @@ class PanelBatch(ctypes.Structure):
                 ("mrkv_hist", vp)]
 
 
+class StationaryModel(ctypes.Structure):
+    _fields_ = [("n_cal", ctypes.c_int32), ("S", ctypes.c_int32), ("n_a", ctypes.c_int32)] + \
+               [(n, vp) for n in ("a_grid", "P", "lab", "beta", "crra", "alpha", "delta", "disc")]
+
+
+class GeOptions(ctypes.Structure):
+    _fields_ = [("method", ctypes.c_int32), ("r_tol", ctypes.c_double), ("egm_tol", ctypes.c_double),
+                ("hist_tol", ctypes.c_double), ("max_steps", ctypes.c_int32), ("max_egm_cycles", ctypes.c_int32),
+                ("max_hist_iter", ctypes.c_int32), ("warm_hist", ctypes.c_int32), ("warm_egm", ctypes.c_int32),
+                ("accel", ctypes.c_int32), ("r_lo", vp), ("r_hi", vp)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "aiy_version": (ctypes.c_int32, []),
@@ -88,6 +101,14 @@ SIGNATURES = {
                                               vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, vp, vp]),
     "aiy_sim_period_prices": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market),
                                                ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
+    "aiy_get_shocks": (ctypes.c_int32, [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp,
+                                        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, vp]),
+    "aiy_get_states": (ctypes.c_int32, [vp, vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double, vp, vp, vp, vp,
+                                        vp]),
+    "aiy_get_controls": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, c_double_p,
+                                          ctypes.c_int32, ctypes.c_double, ctypes.c_int64, vp, vp, vp, vp, vp]),
+    "aiy_get_poststates": (ctypes.c_int32, [vp, ctypes.c_int64, vp, vp, vp, vp]),
+    "aiy_sum": (ctypes.c_int32, [vp, vp, ctypes.c_int64, vp, vp]),
     "aiy_sim_kernel_time": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
                                              vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), vp]),
@@ -113,6 +134,9 @@ SIGNATURES = {
                                         ctypes.c_double, ctypes.c_int32, ctypes.c_int32, vp, vp, c_double_p,
                                         c_int32_p, vp]),
     "aiy_hist_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
+    "aiy_ge_stationary_work_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "aiy_ge_stationary": (ctypes.c_int32, [vp, ctypes.POINTER(StationaryModel), ctypes.POINTER(GeOptions), vp,
+                                           c_double_p, c_double_p, c_double_p, c_int32_p, c_int32_p, c_int32_p, vp]),
     "aiy_wealth_stats": (ctypes.c_int32, [vp, vp, vp, ctypes.c_int64, c_double_p, ctypes.c_int32, c_double_p,
                                           c_double_p, vp]),
 }

@@ -344,7 +344,7 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
   return AIY_OK;
 }
 
-static int32_t egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
                               int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
                               double* work_m, double* work_c, double* m_out, double* c_out, int32_t* cycles_out,
                               double* dist_out, aiy_stream stream) {
@@ -421,7 +421,7 @@ static int32_t egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy
 extern "C" int32_t aiy_egm_solve(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
                                  int32_t max_cycles, int32_t chunk, double* work_m, double* work_c, double* m_out,
                                  double* c_out, int32_t* cycles_out, double* dist_out, aiy_stream stream) {
-  return egm_solve_impl(h, dims, in, tol, max_cycles, chunk, nullptr, nullptr, work_m, work_c, m_out, c_out,
+  return aiy_egm_solve_impl(h, dims, in, tol, max_cycles, chunk, nullptr, nullptr, work_m, work_c, m_out, c_out,
                         cycles_out, dist_out, stream);
 }
 
@@ -430,7 +430,7 @@ extern "C" int32_t aiy_egm_solve_from(aiy_handle* h, const aiy_egm_dims* dims, c
                                       double* work_m, double* work_c, double* m_out, double* c_out,
                                       int32_t* cycles_out, double* dist_out, aiy_stream stream) {
   if (h && (!m_init || !c_init)) return fail(h, AIY_ERR_ARG, "null initial tables");
-  return egm_solve_impl(h, dims, in, tol, max_cycles, chunk, m_init, c_init, work_m, work_c, m_out, c_out,
+  return aiy_egm_solve_impl(h, dims, in, tol, max_cycles, chunk, m_init, c_init, work_m, work_c, m_out, c_out,
                         cycles_out, dist_out, stream);
 }
 

@@ -1,0 +1,229 @@
+// General equilibrium of the stationary Aiyagari household (build-defined row E1) as ONE
+// library call: the root search on r of K_s(r) = K_d(r) for every calibration of a batch,
+// each K_s(r) evaluated on device (stationary EGM -> Young lottery -> device-resident
+// distribution iteration -> K reduction), the brackets moved on the host between the
+// evaluations (a handful of doubles per calibration and step).
+//
+//   w(r) = (1 - alpha) (alpha / (r + delta))^(alpha / (1 - alpha)),  R = 1 + r
+//   K_d(r) = (alpha / (r + delta))^(1 / (1 - alpha))           (calc_R_and_W's firm, L = 1)
+//
+// Methods: 0 = bisection (oracle/stationary.py ge_bisect, step for step); 1 = bisection
+// until both signs of K_s - K_d are evaluated, then Brent's method per calibration (the
+// scipy.optimize.brentq algorithm; aiyagari_hark_amd/stationary.py _Brent is the same
+// coroutine in Python).
+#include "common.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+namespace aiy {
+
+// one calibration's root search (bisect-to-a-sign-change, then brentq)
+struct RootSearch {
+  double lo, hi, xtol;
+  bool have_lo = false, have_hi = false, brent = false, done = false;
+  double flo = 0, fhi = 0, x = 0;
+  double xpre = 0, fpre = 0, xcur = 0, fcur = 0, xblk = 0, fblk = 0, spre = 0, scur = 0;
+  double xprev_eval = 0, fprev_eval = 0;
+  int method = 1;
+
+  void init(double l, double h, double tol, int meth) {
+    lo = l; hi = h; xtol = tol; method = meth;
+    x = 0.5 * (lo + hi);
+    done = !(hi - lo > xtol);
+  }
+  void update(double f) {
+    if (done) return;
+    if (method == 0) {   // oracle ge_bisect: Ks > Kd -> hi = mid
+      if (f > 0) hi = x; else lo = x;
+      if (!(hi - lo > xtol)) { done = true; x = 0.5 * (lo + hi); return; }
+      x = 0.5 * (lo + hi);
+      return;
+    }
+    if (!brent) {
+      if (f > 0) { hi = x; fhi = f; have_hi = true; } else { lo = x; flo = f; have_lo = true; }
+      if (hi - lo <= xtol) { done = true; x = 0.5 * (lo + hi); return; }
+      if (!have_lo || !have_hi) { x = 0.5 * (lo + hi); return; }
+      brent = true;
+      xpre = lo; fpre = flo; xcur = hi; fcur = fhi;
+      xblk = fblk = spre = scur = 0.0;
+      step();
+      return;
+    }
+    xpre = xprev_eval; fpre = fprev_eval; fcur = f;
+    step();
+  }
+  void step() {
+    if (fpre * fcur < 0) { xblk = xpre; fblk = fpre; spre = scur = xcur - xpre; }
+    if (std::fabs(fblk) < std::fabs(fcur)) {
+      const double xp = xcur, xc = xblk, fp = fcur, fc = fblk;
+      xpre = xp; xcur = xc; xblk = xp;
+      fpre = fp; fcur = fc; fblk = fp;
+    }
+    const double delta = 0.5 * (xtol + 4 * DBL_EPSILON * std::fabs(xcur));
+    const double sbis = 0.5 * (xblk - xcur);
+    if (fcur == 0 || std::fabs(sbis) < delta) { done = true; x = xcur; return; }
+    if (std::fabs(spre) > delta && std::fabs(fcur) < std::fabs(fpre)) {
+      double stry;
+      if (xpre == xblk) {
+        stry = -fcur * (xcur - xpre) / (fcur - fpre);
+      } else {
+        const double dpre = (fpre - fcur) / (xpre - xcur);
+        const double dblk = (fblk - fcur) / (xblk - xcur);
+        stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
+      }
+      if (2 * std::fabs(stry) < std::min(std::fabs(spre), 3 * std::fabs(sbis) - delta)) { spre = scur; scur = stry; }
+      else { spre = sbis; scur = sbis; }
+    } else {
+      spre = sbis; scur = sbis;
+    }
+    xprev_eval = xcur; fprev_eval = fcur;
+    xcur += std::fabs(scur) > delta ? scur : (sbis > 0 ? delta : -delta);
+    x = xcur;
+  }
+};
+
+__global__ void fill_prices_kernel(int n_cal, int S, const double* __restrict__ R, const double* __restrict__ w,
+                                   double* __restrict__ Rn, double* __restrict__ Wn, double* __restrict__ Mn) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_cal * S) return;
+  const int c = q / S;
+  Rn[q] = R[c];
+  Wn[q] = w[c];
+  Mn[q] = 0.0;
+}
+
+__global__ void fill_value_kernel(double* x, long long n, double v) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) x[q] = v;
+}
+
+struct GeLayout {
+  size_t Rn, Wn, Mn, Mg, Rc, wc, tm, tc, wm, wc2, lo, wlo, mass, hw, bytes;
+};
+static GeLayout ge_layout(int n_cal, int S, int n_a) {
+  GeLayout L;
+  const size_t ns = (size_t)n_cal * S, tab = ns * (n_a + 1), pts = ns * n_a;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
+  L.Rn = take(ns * 8); L.Wn = take(ns * 8); L.Mn = take(ns * 8); L.Mg = take((size_t)n_cal * 8);
+  L.Rc = take((size_t)n_cal * 8); L.wc = take((size_t)n_cal * 8);
+  L.tm = take(tab * 8); L.tc = take(tab * 8); L.wm = take(2 * tab * 8); L.wc2 = take(2 * tab * 8);
+  L.lo = take(pts * 4); L.wlo = take(pts * 8); L.mass = take(pts * 8); L.hw = take(2 * pts * 8);
+  L.bytes = o;
+  return L;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" int64_t aiy_ge_stationary_work_bytes(int32_t n_cal, int32_t S, int32_t n_a) {
+  if (n_cal < 1 || S < 1 || n_a < 2) return -1;
+  return (int64_t)ge_layout(n_cal, S, n_a).bytes;
+}
+
+extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* M, const aiy_ge_options* o,
+                                     void* work, double* r_out, double* K_out, double* Ks_out, int32_t* steps_out,
+                                     int32_t* egm_cycles_out, int32_t* hist_iters_out, aiy_stream stream) {
+  if (!h) return AIY_ERR_ARG;
+  if (!M || !o || !work || !r_out || !K_out) return fail(h, AIY_ERR_ARG, "null argument");
+  const int n_cal = M->n_cal, S = M->S, n_a = M->n_a;
+  if (n_cal < 1 || S < 1 || S > AIY_MAX_STATES || n_a < 2) return fail(h, AIY_ERR_ARG, "bad sizes");
+  if (!M->a_grid || !M->P || !M->lab || !M->beta || !M->crra || !M->alpha || !M->delta || !M->disc)
+    return fail(h, AIY_ERR_ARG, "null model array");
+  if (o->method != 0 && o->method != 1) return fail(h, AIY_ERR_ARG, "method must be 0 (bisect) or 1 (brent)");
+  if (!(o->r_tol > 0) || o->max_steps < 1) return fail(h, AIY_ERR_ARG, "bad r_tol / max_steps");
+  AIY_HIP(h, hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  AIY_USE_STREAM(h, st);
+  const GeLayout L = ge_layout(n_cal, S, n_a);
+  char* base = static_cast<char*>(work);
+  double* Rn = reinterpret_cast<double*>(base + L.Rn);
+  double* Wn = reinterpret_cast<double*>(base + L.Wn);
+  double* Mn = reinterpret_cast<double*>(base + L.Mn);
+  double* Mg = reinterpret_cast<double*>(base + L.Mg);
+  double* Rc = reinterpret_cast<double*>(base + L.Rc);
+  double* wc = reinterpret_cast<double*>(base + L.wc);
+  double* tm = reinterpret_cast<double*>(base + L.tm);
+  double* tc = reinterpret_cast<double*>(base + L.tc);
+  double* wm = reinterpret_cast<double*>(base + L.wm);
+  double* wc2 = reinterpret_cast<double*>(base + L.wc2);
+  int32_t* lo = reinterpret_cast<int32_t*>(base + L.lo);
+  double* wlo = reinterpret_cast<double*>(base + L.wlo);
+  double* mass = reinterpret_cast<double*>(base + L.mass);
+  double* hw = reinterpret_cast<double*>(base + L.hw);
+  AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
+
+  std::vector<RootSearch> rs(n_cal);
+  for (int c = 0; c < n_cal; ++c) {
+    const double lo0 = o->r_lo ? o->r_lo[c] : -0.5 * M->delta[c];
+    const double hi0 = o->r_hi ? o->r_hi[c] : 1.0 / M->disc[c] - 1.0 - 1e-9;
+    rs[c].init(lo0, hi0, o->r_tol, o->method);
+  }
+  std::vector<double> R(n_cal), w(n_cal), Kd(n_cal), Ks(n_cal, 0.0);
+  std::vector<int32_t> cyc(n_cal), its(n_cal);
+  std::vector<double> dist(n_cal);
+  aiy_egm_dims dims{n_cal, S, 1, n_a};
+  aiy_egm_inputs in{M->a_grid, Mg, M->P, Rn, Wn, Mn, M->lab, M->beta, M->crra};
+  const int saved_accel = h->hist_accel;
+  int steps = 0;
+  int32_t rc = AIY_OK;
+  long long cyc_sum = 0, it_sum = 0;
+  while (steps < o->max_steps) {
+    bool all_done = true;
+    for (int c = 0; c < n_cal; ++c) all_done = all_done && rs[c].done;
+    if (all_done) break;
+    for (int c = 0; c < n_cal; ++c) {
+      const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];
+      const double KtoL = std::pow(a / (r + d), 1.0 / (1.0 - a));
+      R[c] = 1.0 + r;
+      w[c] = (1.0 - a) * std::pow(KtoL, a);
+      Kd[c] = KtoL;
+    }
+    AIY_HIP(h, hipMemcpyAsync(Rc, R.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+    AIY_HIP(h, hipMemcpyAsync(wc, w.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(fill_prices_kernel, dim3((n_cal * S + 255) / 256), dim3(256), 0, st, n_cal, S, Rc, wc, Rn, Wn,
+                       Mn);
+    AIY_CHECK_LAUNCH(h);
+    const bool warm_egm = o->warm_egm && steps > 0;
+    rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, 32,
+                            warm_egm ? tm : nullptr, warm_egm ? tc : nullptr, wm, wc2, tm, tc, cyc.data(), dist.data(),
+                            stream);
+    if (rc) break;
+    rc = aiy_hist_lottery(h, n_cal, S, n_a, tm, tc, M->a_grid, Rc, wc, M->lab, lo, wlo, stream);
+    if (rc) break;
+    if (!(o->warm_hist && steps > 0)) {
+      const long long n = (long long)n_cal * S * n_a;
+      hipLaunchKernelGGL(fill_value_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, mass, n,
+                         1.0 / ((double)S * n_a));
+      AIY_CHECK_LAUNCH(h);
+    }
+    h->hist_accel = o->accel;
+    rc = aiy_hist_solve(h, n_cal, S, n_a, lo, wlo, M->P, M->a_grid, o->hist_tol,
+                        o->max_hist_iter > 0 ? o->max_hist_iter : 200000, 64, mass, hw, Ks.data(), its.data(), stream);
+    h->hist_accel = saved_accel;
+    if (rc) break;
+    for (int c = 0; c < n_cal; ++c) {
+      cyc_sum += cyc[c];
+      it_sum += its[c];
+      rs[c].update(Ks[c] - Kd[c]);
+    }
+    ++steps;
+  }
+  h->hist_accel = saved_accel;
+  if (rc) return rc;
+  for (int c = 0; c < n_cal; ++c) {
+    const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];
+    r_out[c] = r;
+    K_out[c] = std::pow(a / (r + d), 1.0 / (1.0 - a));
+    if (Ks_out) Ks_out[c] = Ks[c];
+  }
+  if (steps_out) *steps_out = steps;
+  if (egm_cycles_out) *egm_cycles_out = (int32_t)std::min<long long>(cyc_sum, 0x7fffffff);
+  if (hist_iters_out) *hist_iters_out = (int32_t)std::min<long long>(it_sum, 0x7fffffff);
+  return AIY_OK;
+}

@@ -6,8 +6,8 @@
 // CLUSTER of G workgroups (one per CU) that iterates on its own, synchronised by a
 // per-calibration counter instead of kernel boundaries:
 //   * workgroup w of a cluster owns asset columns [j0, j1) of every income state: the
-//     mass of those columns lives in REGISTERS for the whole solve (thread t holds column
-//     j0 + t, all S states);
+//     mass of those columns lives in REGISTERS for the whole solve (thread t holds columns
+//     j0 + t + k * TH, all S states; with S <= 8 also their lottery);
 //   * push (sources = own columns): T_s[lo] += w m, T_s[lo + 1] += (1 - w) m, accumulated
 //     with LDS f64 atomics into a per-row destination SPAN buffer: a monotone lottery maps
 //     the contiguous source range to the contiguous destination range
@@ -17,7 +17,7 @@
 //   * gather (destinations = own columns): T_s[d] = sum of the slabs whose span covers d
 //     (the covering workgroups are fixed for the whole solve and found once at start), in
 //     ascending workgroup order, every load of a row group issued before the first use;
-//   * mix: mass'[s'][d] = sum_s P[s, s'] T_s[d] (P in LDS); the sup-norm change is reduced
+//   * mix: mass'[s'][d] = sum_s P[s, s'] T_s[d] (P broadcast from LDS); the sup-norm change is reduced
 //     to one published value per workgroup, read by the cluster after the NEXT barrier:
 //     the solve stops exactly where oracle/stationary.py stationary_hist stops (first
 //     iteration with max |mass' - mass| < tol) and keeps that iteration's mass.
@@ -37,9 +37,9 @@ constexpr int kHcMaxG = 128;                       // workgroups per calibration
 constexpr int kHcCand = 32;                        // covering workgroups per (row, workgroup)
 constexpr int kHcRows = 8;                         // rows whose push loads are in flight together
 // rows whose gather loads are in flight together: all (S <= 8) for one column per thread
-template <int SMAX, int KC>
+template <int SMAX, int KC, int TH>
 struct HcGather {
-  static constexpr int kRows = (SMAX == 8 && KC == 1) ? 8 : 4;
+  static constexpr int kRows = SMAX == 8 ? 8 : 4;
 };
 constexpr size_t kHcLdsTotal = 160 * 1024;         // per CU
 constexpr unsigned long long kHcTimeoutTicks = 200000000ull;   // 2 s of the 100 MHz clock
@@ -54,7 +54,9 @@ struct HcRun {
   double* slab;           // [launch cals][G][2][cap]
   int* span;              // [launch cals][G][SMAX][2] (first, len)
   unsigned* ctr;          // [launch cals][kHcCtrStride]
-  unsigned long long* dist;   // [launch cals][2][G]
+  double* dist;           // [launch cals][2][G][4]: sup-norm change, Aitken dot products, valid
+  double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0)
+  int accel;              // Aitken extrapolation period E (0: plain iteration = the oracle's)
   int* iters_out;         // [n_cal]
   unsigned* err;          // 0 ok, 1 timeout, 2 span overflow / not monotone, 3 candidate overflow
   double tol;
@@ -90,7 +92,7 @@ __device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsign
 #ifdef AIY_DIAG_PHASES
 #define HC_PH(k)                                                        \
   do {                                                                  \
-    if (tid == 0 && blockIdx.x == 0) {                                  \
+    if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES) {                    \
       const unsigned long long tn = __builtin_amdgcn_s_memrealtime();   \
       if (k) ph[k - 1] += tn - tq;                                      \
       tq = tn;                                                          \
@@ -123,16 +125,18 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
 template <int SMAX, int KC, int TH>
 __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 #ifdef AIY_DIAG_PHASES
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tq = 0;
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = 0;
 #endif
   extern __shared__ double Tacc[];                 // destination spans of this workgroup
-  __shared__ double sP[SMAX * SMAX];
   __shared__ int s_first[SMAX], s_off[SMAX + 1];
   __shared__ HcCand s_cand[SMAX][kHcCand];
   __shared__ int s_ncand[SMAX];
   __shared__ double s_red[TH / kWave];
   __shared__ int s_cinfo[KC * SMAX * TH];
   __shared__ int s_flag, s_stop;
+  __shared__ double s_dot[2][TH / kWave];
+  __shared__ double s_lam[2], s_fext;
+  __shared__ double s_P[SMAX * SMAX];              // P[s][s'] zero-padded to SMAX x SMAX
 
   const int tid = threadIdx.x;
   const int G = r.G, S = r.S, n_a = r.n_a, cap = r.cap;
@@ -142,16 +146,22 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
   const int j0 = w * r.nj;
   const int j1 = min(j0 + r.nj, n_a);
   unsigned* ctr = r.ctr + (size_t)lc * kHcCtrStride;
-  unsigned long long* dist = r.dist + (size_t)lc * 2 * G;
+  double* dist = r.dist + (size_t)lc * 2 * G * 4;
+  double* DB = r.dbuf ? r.dbuf + (size_t)cal * S * n_a : nullptr;
+  const int E = r.accel;
   const size_t row0 = (size_t)cal * S;
   const int* LO = r.lo + row0 * n_a;
   const double* WL = r.wlo + row0 * n_a;
   double* MS = r.mass + row0 * n_a;
   double* slab_cl = r.slab + (size_t)lc * G * 2 * cap;
+  const double* __restrict__ Pc = r.P + (size_t)cal * S * S;
   int* span_cl = r.span + (size_t)lc * G * SMAX * 2;
 
   // ---- setup: P, own spans, mass -> registers ----
-  for (int q = tid; q < S * S; q += TH) sP[q] = r.P[(size_t)cal * S * S + q];
+  for (int q = tid; q < SMAX * SMAX; q += TH) {
+    const int s = q / SMAX, sp = q - s * SMAX;
+    s_P[q] = (s < S && sp < S) ? Pc[s * S + sp] : 0.0;
+  }
   if (tid == 0) {
     int tot = 0;
     unsigned bad = 0;
@@ -233,11 +243,33 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 
   const int lane = tid & (kWave - 1);
   double dloc = 0.0;   // this workgroup's sup-norm change of the last mix
+  double aloc = 0.0, bloc = 0.0, vloc = 0.0;   // Aitken dot products of the last mix, valid flag
   int final_it = 0;
+  if (tid == 0) {
+    s_lam[0] = s_lam[1] = -1.0;
+    s_fext = 0.0;
+  }
+  // the lottery (lo, weight) of the own columns is fixed for the whole solve: with S <= 8
+  // it is held in registers, loaded once (larger S re-read it from L2 every iteration)
+  constexpr bool kLoReg = SMAX == 8;
+  int dreg[KC][kLoReg ? SMAX : 1];
+  double wreg[KC][kLoReg ? SMAX : 1];
+  if constexpr (kLoReg) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = j0 + tid + k * TH;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const bool ok = s < S && j < j1;
+        dreg[k][s] = ok ? LO[(size_t)s * n_a + j] : -1;
+        wreg[k][s] = ok ? WL[(size_t)s * n_a + j] : 0.0;
+      }
+    }
+  }
   for (int it = 1; it <= r.max_iter; ++it) {
     const int par = it & 1;
     HC_PH(0);
-    // ---- push own sources into the span buffer (row groups: loads in flight together) ----
+    // ---- push own sources into the span buffer ----
 #pragma unroll
     for (int s0 = 0; s0 < SMAX; s0 += kHcRows) {
       if (s0 < S) {
@@ -249,16 +281,21 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 #pragma unroll
           for (int q = 0; q < kHcRows; ++q) {
             const int s = s0 + q;
-            const bool ok = s < S && j < j1;
-            dd[k][q] = ok ? LO[(size_t)s * n_a + j] : -1;
-            ww[k][q] = ok ? WL[(size_t)s * n_a + j] : 0.0;
+            if constexpr (kLoReg) {
+              dd[k][q] = dreg[k][s];
+              ww[k][q] = wreg[k][s];
+            } else {
+              const bool ok = s < S && j < j1;
+              dd[k][q] = ok ? LO[(size_t)s * n_a + j] : -1;
+              ww[k][q] = ok ? WL[(size_t)s * n_a + j] : 0.0;
+            }
           }
         }
         // one LDS f64 atomic per lane and destination: adjacent lanes hit adjacent
-        // destinations (no conflict) except on the borrowing constraint, where the LDS
-        // serialises same-address adds at a few cycles each -- cheaper than a wave
-        // segmented scan, whose dependent cross-lane steps cost ~1.4k cycles per row
-        // (measured at Table II size: 17 us per iteration for the push with the scan)
+        // destinations (no conflict) except on the borrowing constraint, where the whole
+        // wave shares one destination and a DPP wave sum replaces 64 same-address atomics
+        // (a general segmented scan costs ~1.4k cycles of dependent cross-lane steps per
+        // row: measured 17 us per iteration for the push at Table II size)
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
           const bool act = j0 + tid + k * TH < j1;
@@ -272,8 +309,6 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
               const int base = s_off[s] - s_first[s];
               const int d0 = __builtin_amdgcn_readfirstlane(d);
               if (__all(act && d == d0)) {
-                // one destination for the whole wave (the borrowing constraint): a DPP
-                // wave sum and one atomic instead of 64 same-address LDS atomics
                 const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
                 if (lane == kWave - 1) {
                   atomicAdd(&Tacc[base + d0], tl);
@@ -296,39 +331,35 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       store_f64_agent(&slab[q], Tacc[q]);
       Tacc[q] = 0.0;
     }
-    if (tid == 0)   // the previous mix's change (iteration it - 1)
-      store_u64_agent(&dist[(size_t)((it - 1) & 1) * G + w], (unsigned long long)__double_as_longlong(dloc));
+    if (tid == 0) {   // the previous mix's change (iteration it - 1) and its Aitken products
+      double* dp = &dist[((size_t)((it - 1) & 1) * G + w) * 4];
+      store_f64_agent(&dp[0], dloc);
+      store_f64_agent(&dp[1], aloc);
+      store_f64_agent(&dp[2], bloc);
+      store_f64_agent(&dp[3], vloc);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     HC_PH(2);
     if (!hc_barrier(r, ctr, (unsigned)(it + 2) * G, &s_flag)) return;
     HC_PH(3);
-    // ---- stop where the oracle stops: max change of iteration it - 1 < tol ----
-    if (it >= 2) {
-      if (tid < kWave) {
-        double d = 0.0;
-        for (int w2 = lane; w2 < G; w2 += kWave)
-          d = nan_max(d, __longlong_as_double((long long)load_u64_agent(&dist[(size_t)((it - 1) & 1) * G + w2])));
-        d = wave_nan_max(d);
-        if (tid == 0) s_stop = (d < r.tol) ? 1 : 0;
-      }
-      __syncthreads();
-      if (s_stop) {
-        final_it = it - 1;
-        break;
-      }
-    }
-    // ---- gather own destinations from the covering slabs (ascending w), mix ----
+    // ---- gather own destinations from the covering slabs (ascending w); the stop check
+    // runs while the first row group's loads are in flight ----
+    constexpr int GR = HcGather<SMAX, KC, TH>::kRows;
     double T[KC][SMAX];
 #pragma unroll
-    for (int s0 = 0; s0 < SMAX; s0 += (HcGather<SMAX, KC>::kRows)) {
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) T[k][s] = 0.0;   // rows beyond S stay 0 (padded mix)
+    bool more = false;
+#pragma unroll
+    for (int s0 = 0; s0 < SMAX; s0 += GR) {
       if (s0 < S) {
-        double v0[KC][(HcGather<SMAX, KC>::kRows)], v1[KC][(HcGather<SMAX, KC>::kRows)];
-        bool more = false;
+        double v0[KC][GR], v1[KC][GR];
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
           const int d = j0 + tid + k * TH;
 #pragma unroll
-          for (int q = 0; q < (HcGather<SMAX, KC>::kRows); ++q) {
+          for (int q = 0; q < GR; ++q) {
             const int s = s0 + q;
             v0[k][q] = 0.0;
             v1[k][q] = 0.0;
@@ -346,96 +377,158 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
             }
           }
         }
-        // columns covered by > 2 spans (the borrowing constraint): their extra loads are
-        // issued together, before the first use
-        double v2[KC][(HcGather<SMAX, KC>::kRows)], v3[KC][(HcGather<SMAX, KC>::kRows)];
-        bool more4 = false;
-        if (__any(more)) {
+        if (s0 == 0 && it >= 2) {
+          // stop where the oracle stops: max change of iteration it - 1 < tol
+          if (tid < kWave) {
+            // every workgroup's (change, dot products, valid) of mix it - 1: all loads of
+            // the wave in flight together (kHcMaxG <= 2 * 64 workgroups)
+            const double* dq = &dist[(size_t)((it - 1) & 1) * G * 4];
+            double xd[2], xa[2], xb[2], xv[2];
 #pragma unroll
-          for (int k = 0; k < KC; ++k) {
-            const int d = j0 + tid + k * TH;
-#pragma unroll
-            for (int q = 0; q < (HcGather<SMAX, KC>::kRows); ++q) {
-              const int s = s0 + q;
-              v2[k][q] = 0.0;
-              v3[k][q] = 0.0;
-              if (s < S) {
-                const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
-                if (cn >= 3) {
-                  const HcCand c2 = s_cand[s][cf + 2];
-                  v2[k][q] = load_f64_agent(&slab_cl[((size_t)c2.w * 2 + par) * cap + c2.off + d - c2.first]);
-                }
-                if (cn >= 4) {
-                  const HcCand c3 = s_cand[s][cf + 3];
-                  v3[k][q] = load_f64_agent(&slab_cl[((size_t)c3.w * 2 + par) * cap + c3.off + d - c3.first]);
-                }
-                more4 = more4 || cn > 4;
+            for (int u = 0; u < 2; ++u) {
+              const int w2 = lane + u * kWave;
+              const bool ok = w2 < G;
+              xd[u] = ok ? load_f64_agent(&dq[w2 * 4 + 0]) : 0.0;
+              xa[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 1]) : 0.0;
+              xb[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 2]) : 0.0;
+              xv[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 3]) : 0.0;
+            }
+            const double dd2 = wave_nan_max(nan_max(xd[0], xd[1]));
+            // fixed-order sums over the workgroups (lane pairs, then the DPP tree)
+            const double asum = wave_sum_lane63(xa[0] + xa[1]);
+            const double bsum = wave_sum_lane63(xb[0] + xb[1]);
+            const double valid = xv[0];
+            if (lane == kWave - 1) {
+              s_dot[0][0] = asum;
+              s_dot[1][0] = bsum;
+            }
+            if (tid == 0) {
+              s_stop = (dd2 < r.tol) ? 1 : 0;
+              s_red[0] = valid;
+            }
+          }
+          __syncthreads();
+          if (tid == 0) {
+            {
+              // Aitken: the cluster's dot products of mix it - 1
+              if (E > 0 && s_red[0] != 0.0) {
+                const double a = s_dot[0][0], b = s_dot[1][0];
+                const int ph = (it - 1) % E;           // E - 1: first estimate, 0: second
+                s_lam[ph == 0 ? 1 : 0] = b > 0.0 ? a / b : -1.0;
+              }
+              s_fext = 0.0;
+              if (E > 0 && it > E && it % E == 1) {
+                const double l0 = s_lam[0], l1 = s_lam[1];
+                if (l1 > 0.5 && l1 < 1.0 - 1e-9 && fabs(l1 - l0) < 1e-3 * (1.0 - l1)) s_fext = l1 / (1.0 - l1);
+                s_lam[0] = s_lam[1] = -1.0;
               }
             }
           }
-        } else {
-#pragma unroll
-          for (int k = 0; k < KC; ++k)
-#pragma unroll
-            for (int q = 0; q < (HcGather<SMAX, KC>::kRows); ++q) v2[k][q] = v3[k][q] = 0.0;
+          __syncthreads();
         }
 #pragma unroll
         for (int k = 0; k < KC; ++k)
 #pragma unroll
-          for (int q = 0; q < (HcGather<SMAX, KC>::kRows); ++q)
-            if (s0 + q < SMAX) T[k][s0 + q] = ((v0[k][q] + v1[k][q]) + v2[k][q]) + v3[k][q];
-        if (more4) {   // > 4 covering spans: rare, serial
+          for (int q = 0; q < GR; ++q) T[k][s0 + q] = v0[k][q] + v1[k][q];
+      }
+    }
+    if (it >= 2 && s_stop) {
+      final_it = it - 1;
+      break;
+    }
+    HC_PH(4);
+    if (__any(more)) {   // columns covered by > 2 spans (the borrowing constraint)
 #pragma unroll
-          for (int k = 0; k < KC; ++k) {
-            const int d = j0 + tid + k * TH;
+      for (int k = 0; k < KC; ++k) {
+        const int d = j0 + tid + k * TH;
 #pragma unroll
-            for (int q = 0; q < (HcGather<SMAX, KC>::kRows); ++q) {
-              const int s = s0 + q;
-              if (s < S) {
-                const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
-                for (int c = 4; c < cn; ++c) {
+        for (int s = 0; s < SMAX; ++s) {
+          if (s < S) {
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+            for (int c0 = 2; c0 < cn; c0 += 4) {   // four loads in flight per step
+              double x[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u;
+                x[u] = 0.0;
+                if (c < cn) {
                   const HcCand cx = s_cand[s][cf + c];
-                  T[k][s] += load_f64_agent(&slab_cl[((size_t)cx.w * 2 + par) * cap + cx.off + d - cx.first]);
+                  x[u] = load_f64_agent(&slab_cl[((size_t)cx.w * 2 + par) * cap + cx.off + d - cx.first]);
                 }
               }
+              T[k][s] += ((x[0] + x[1]) + x[2]) + x[3];
             }
           }
         }
       }
     }
-    HC_PH(4);
-    double dmax = 0.0;
+    HC_PH(5);
+    // Aitken phases of this mix (it % E): E - 2 store the difference; E - 1 and 0 form the
+    // dot products <d_it, d_it-1>, |d_it-1|^2 of two consecutive ratio estimates; at 1 the
+    // cluster may extrapolate along d_it (s_fext, decided above from those two estimates)
+    const int aph = E > 0 ? it % E : -1;
+    const bool a_store = E > 0 && (aph == E - 2 || aph == E - 1);
+    const bool a_dot = E > 0 && it >= E - 1 && (aph == E - 1 || aph == 0);
+    const double fext = s_fext;
+    double dmax = 0.0, ap = 0.0, bp = 0.0;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
-      const bool act = j0 + tid + k * TH < j1;
+      const int j = j0 + tid + k * TH;
+      const bool act = j < j1;
 #pragma unroll
       for (int sp = 0; sp < SMAX; ++sp) {
         if (sp < S) {
           double acc = 0.0;
 #pragma unroll
-          for (int s = 0; s < SMAX; ++s)
-            if (s < S) acc += sP[s * S + sp] * T[k][s];   // P.T @ T
-          if (act) dmax = nan_max(dmax, fabs(acc - m[k][sp]));
-          m[k][sp] = acc;
+          for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * T[k][s];   // P.T @ T (LDS broadcast; T = 0 beyond S)
+          const double dnew = acc - m[k][sp];
+          if (act) {
+            dmax = nan_max(dmax, fabs(dnew));
+            if (a_dot) {   // 2 of every E iterations: the load latency does not matter
+              const double dprev = DB[(size_t)sp * n_a + j];
+              ap += dnew * dprev;
+              bp += dprev * dprev;
+            }
+            if (a_store) DB[(size_t)sp * n_a + j] = dnew;
+          }
+          m[k][sp] = fext != 0.0 ? acc + fext * dnew : acc;   // x* ~ x + d lambda / (1 - lambda)
         }
       }
     }
+    HC_PH(6);
     dmax = wave_nan_max(dmax);
     if (lane == 0) s_red[tid / kWave] = dmax;
+    if (a_dot) {
+      ap = wave_sum_lane63(ap);
+      bp = wave_sum_lane63(bp);
+      if (lane == kWave - 1) {
+        s_dot[0][tid / kWave] = ap;
+        s_dot[1][tid / kWave] = bp;
+      }
+    }
     __syncthreads();
     if (tid == 0) {
       double d = s_red[0];
       for (int q = 1; q < TH / kWave; ++q) d = nan_max(d, s_red[q]);
       dloc = d;
+      aloc = bloc = 0.0;
+      vloc = a_dot ? 1.0 : 0.0;
+      if (a_dot)
+        for (int q = 0; q < TH / kWave; ++q) {
+          aloc += s_dot[0][q];
+          bloc += s_dot[1][q];
+        }
     }
-    HC_PH(5);
+    HC_PH(7);
     final_it = it;
   }
 #ifdef AIY_DIAG_PHASES
-  if (tid == 0 && blockIdx.x == 0 && final_it > 0)
-    printf("[hist phases] G=%d nj=%d iters=%d us/iter: push %.2f publish %.2f barrier %.2f check+gather %.2f mix %.2f\n",
-           G, r.nj, final_it, ph[0] * 0.01 / final_it, ph[1] * 0.01 / final_it, ph[2] * 0.01 / final_it,
-           ph[3] * 0.01 / final_it, ph[4] * 0.01 / final_it);
+  if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES && final_it > 0)
+    printf("[hist phases] block %d G=%d nj=%d iters=%d us/iter: push %.2f publish %.2f barrier %.2f check+gather %.2f "
+           "heavy %.2f mix %.2f reduce %.2f\n",
+           (int)blockIdx.x, G, r.nj, final_it, ph[0] * 0.01 / final_it, ph[1] * 0.01 / final_it,
+           ph[2] * 0.01 / final_it, ph[3] * 0.01 / final_it, ph[4] * 0.01 / final_it, ph[5] * 0.01 / final_it,
+           ph[6] * 0.01 / final_it);
 #endif
   // ---- final mass of the own columns, iteration count ----
 #pragma unroll
@@ -448,24 +541,23 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
   if (w == 0 && tid == 0) r.iters_out[cal] = final_it;
 }
 
-// Host plan of one cluster launch shape: one column per thread (KC = 1) with 512- or
-// 1024-thread workgroups (the 1024 form keeps 16 waves per CU for latency hiding when a
-// workgroup owns more than 512 columns).
+// Host plan of one cluster launch shape: 512-thread workgroups, one or two columns per
+// thread (two only with S <= 8, where the lottery and the mass stay in registers).
 struct HcPlan {
-  int G = 0, nj = 0, th = 0, smax = 0, cals_per_launch = 0, cap = 0;
+  int G = 0, nj = 0, th = 0, kc = 0, smax = 0, cals_per_launch = 0, cap = 0;
   size_t lds = 0;
   const void* fn = nullptr;
 };
 
-template <int SMAX, int TH>
+template <int SMAX, int KC, int TH>
 static const void* hc_fn() {
-  return reinterpret_cast<const void*>(hist_cluster_kernel<SMAX, 1, TH>);
+  return reinterpret_cast<const void*>(hist_cluster_kernel<SMAX, KC, TH>);
 }
 
-static const void* hc_pick(int smax, int th) {
-  if (smax == 8) return th == 512 ? hc_fn<8, 512>() : hc_fn<8, 1024>();
-  if (smax == 16) return hc_fn<16, 512>();
-  return hc_fn<32, 512>();
+static const void* hc_pick(int smax, int kc) {
+  if (smax == 8) return kc == 1 ? hc_fn<8, 1, 512>() : hc_fn<8, 2, 512>();
+  if (smax == 16) return hc_fn<16, 1, 512>();
+  return hc_fn<32, 1, 512>();
 }
 
 static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
@@ -473,18 +565,19 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   p.smax = S <= 8 ? 8 : (S <= 16 ? 16 : 32);
-  const int th_max = p.smax == 8 ? 1024 : 512;
-  const int g_min = (n_a + th_max - 1) / th_max;
+  const int kc_max = p.smax == 8 ? 2 : 1;
+  p.th = 512;
+  const int g_min = (n_a + p.th * kc_max - 1) / (p.th * kc_max);
   if (g_min > kHcMaxG || g_min > cus) return false;
   const int g_cap = h->hist_cluster_cap > 0 ? h->hist_cluster_cap : 32;
   int G = std::max(g_min, std::min(std::min(g_cap, kHcMaxG), cus / std::max(1, n_cal)));
   G = std::min(G, n_a);
   p.nj = (n_a + G - 1) / G;
   p.G = (n_a + p.nj - 1) / p.nj;                    // every workgroup owns >= 1 column
-  p.th = p.nj <= 512 ? 512 : 1024;
-  if (p.th > th_max) return false;
+  p.kc = p.nj <= p.th ? 1 : 2;
+  if (p.kc > kc_max) return false;
   p.cals_per_launch = std::max(1, cus / p.G);
-  p.fn = hc_pick(p.smax, p.th);
+  p.fn = hc_pick(p.smax, p.kc);
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
   const size_t stat = fa.sharedSizeBytes;
@@ -496,7 +589,7 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
 
 static int32_t hc_scratch(aiy_handle* h, int cals, int G, int cap) {
   const size_t need = (size_t)cals * G * 2 * cap * sizeof(double) + (size_t)cals * G * 32 * 2 * sizeof(int) +
-                      (size_t)cals * kHcCtrStride * sizeof(unsigned) + (size_t)cals * 2 * G * sizeof(unsigned long long) +
+                      (size_t)cals * kHcCtrStride * sizeof(unsigned) + (size_t)cals * 2 * G * 4 * sizeof(double) +
                       256;
   if (need > h->hc_cap) {
     if (h->d_hc) (void)hipFree(h->d_hc);
@@ -534,8 +627,22 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   r.ctr = reinterpret_cast<unsigned*>(base + off);
   const size_t ctr_bytes = (size_t)per_launch * kHcCtrStride * sizeof(unsigned);
   off += ctr_bytes;
-  r.dist = reinterpret_cast<unsigned long long*>(base + off);
-  off += (size_t)per_launch * 2 * p.G * sizeof(unsigned long long);
+  r.dist = reinterpret_cast<double*>(base + off);
+  off += (size_t)per_launch * 2 * p.G * 4 * sizeof(double);
+  r.accel = h->hist_accel;
+  r.dbuf = nullptr;
+  if (r.accel > 0) {
+    if (r.accel < 4) r.accel = 4;
+    const size_t db = (size_t)n_cal * S * n_a * sizeof(double);
+    if (db > h->hc_dcap) {
+      if (h->d_hcd) (void)hipFree(h->d_hcd);
+      h->d_hcd = nullptr;
+      h->hc_dcap = 0;
+      AIY_HIP(h, hipMalloc(&h->d_hcd, db));
+      h->hc_dcap = db;
+    }
+    r.dbuf = static_cast<double*>(h->d_hcd);
+  }
   r.err = reinterpret_cast<unsigned*>(base + off);
   for (int c0 = 0; c0 < n_cal; c0 += per_launch) {
     const int nc = std::min(per_launch, n_cal - c0);

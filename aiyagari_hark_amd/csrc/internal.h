@@ -39,6 +39,9 @@ struct aiy_handle {
   bool hist_fused = false;           // AIY_OPT_HIST_FUSED
   bool hist_resident = true;         // AIY_OPT_HIST_RESIDENT (hist_resident.hip)
   int hist_cluster_cap = 0;          // AIY_OPT_HIST_CLUSTER: max workgroups per calibration (0: 32)
+  int hist_accel = 0;                // AIY_OPT_HIST_ACCEL: Aitken period of the resident histogram (0: off)
+  void* d_hcd = nullptr;             // resident histogram: stored differences (Aitken)
+  size_t hc_dcap = 0;
   void* d_hc = nullptr;              // resident histogram: slabs, spans, counters, distances
   size_t hc_cap = 0;
   hipEvent_t hc_ev[2] = {nullptr, nullptr};
@@ -70,6 +73,12 @@ struct aiy_handle {
   bool has_last_stream = false;
   hipEvent_t hand_ev = nullptr;
 };
+
+// EGM solve loop, cold (m_init == NULL) or warm-started (egm.hip).
+int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
+                           int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
+                           double* work_m, double* work_c, double* m_out, double* c_out, int32_t* cycles_out,
+                           double* dist_out, aiy_stream stream);
 
 namespace aiy {
 

@@ -437,6 +437,10 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
     case AIY_OPT_HIST_FUSED: h->hist_fused = value != 0; return AIY_OK;
     case AIY_OPT_RESIDENT_STREAM: h->res_stream = value != 0; return AIY_OK;
     case AIY_OPT_HIST_RESIDENT: h->hist_resident = value != 0; return AIY_OK;
+    case AIY_OPT_HIST_ACCEL:
+      if (value < 0 || value > (1 << 20)) return fail(h, AIY_ERR_ARG, "AIY_OPT_HIST_ACCEL must be >= 0");
+      h->hist_accel = (int)value;
+      return AIY_OK;
     case AIY_OPT_HIST_CLUSTER:
       if (value < 0 || value > 128) return fail(h, AIY_ERR_ARG, "AIY_OPT_HIST_CLUSTER must be in [0, 128]");
       h->hist_cluster_cap = (int)value;

@@ -228,9 +228,100 @@ class AiyagariType:
                 or self.panel.engine != self.panel_engine:
             self.panel = DevicePanel(self.AgentCount, device=self.device, act_T=self.T_sim, engine=self.panel_engine)
         self.lab_cdf = sm.choice_cdf_table(self.TauchenAux[1])          # agent's own chain (AS:1245, Q5)
+        self.state_now["aNow"] = np.full(self.AgentCount, float(self.kInit))   # sim_birth (AS:1213)
+        self._hook_const = None
 
+    # ---- per-period hooks ([HARK] AgentType.simulate / sim_one_period, AS:1161, 1217-1415) ----
+    # One libaiyagari launch per hook over device-resident agent states: the surface a
+    # driver stepping Market.make_history period by period (sow -> cultivate -> reap ->
+    # mill -> store) calls.  AiyagariEconomy.make_history(engine="fused") runs the same
+    # periods as one fused pass; the two agree bit for bit on labour draws.
     def market_action(self):                  # AS:1161
-        raise NotImplementedError("per-period hooks are fused into AiyagariEconomy.make_history on device")
+        self.simulate(1)
+
+    def simulate(self, sim_periods=1):        # [HARK] AgentType.simulate
+        for _ in range(int(sim_periods)):
+            self.sim_one_period()
+
+    def sim_one_period(self):                 # [HARK] AgentType.sim_one_period (no death)
+        self._to_device()
+        for var in self.state_now:
+            self.state_prev[var] = self.state_now[var]
+        self.get_shocks()
+        self.get_states()
+        self.get_controls()
+        self.get_poststates()
+        self.t_sim += 1
+
+    def _to_device(self):
+        """Agent states as device arrays (a: float64, LaborSupplyState / EmpNow: uint8)
+        plus the hooks' constant tables, made once per simulated history."""
+        st, dev, N = self.state_now, self.device, self.AgentCount
+        for k, dt in (("aNow", torch.float64), ("LaborSupplyState", torch.uint8), ("EmpNow", torch.uint8)):
+            if not torch.is_tensor(st[k]):
+                st[k] = torch.as_tensor(np.asarray(st[k]).astype(np.float64 if dt == torch.float64 else np.uint8)
+                                        ).to(dev)
+            if st[k].numel() != N:
+                raise ValueError(f"state {k} holds {st[k].numel()} agents, AgentCount = {N}")
+        if self._hook_const is None:
+            from . import _lib
+            lvl = sm.labor_levels(self.TauchenAux[0])
+            self._hook_const = dict(
+                h=_lib.handle(dev.index if dev.index is not None else torch.cuda.current_device()),
+                lvl=torch.as_tensor(lvl, dtype=torch.float64).to(dev),
+                cdf=torch.as_tensor(self.lab_cdf, dtype=torch.float64).to(dev),
+                n_lab=int(self.lab_cdf.shape[0]))
+
+    def get_shocks(self):                     # AS:1217-1256 (employment fixed: UrateB = UrateG = 0)
+        from . import _lib
+        k = self._hook_const
+        lab = self.state_prev["LaborSupplyState"].clone()
+        u = None
+        if self.shock_mode == "numpy":   # np.random.choice per agent on the global RNG (AS:1254)
+            u = torch.as_tensor(np.random.random_sample(self.AgentCount)).to(self.device)
+        elif self.shock_mode != "philox":
+            raise ValueError(f"shock_mode {self.shock_mode!r}")
+        s = _lib.stream_ptr()
+        k["h"].check(k["h"].lib.aiy_get_shocks(k["h"].h, k["n_lab"], _lib.ptr(k["cdf"]), self.AgentCount, 0,
+                                               _lib.ptr(lab), _lib.ptr(u), int(self.shock_seed) & ((1 << 64) - 1),
+                                               int(getattr(self, "ge_iter", 0)), int(self.t_sim), s), "aiy_get_shocks")
+        self.state_now["LaborSupplyState"] = lab
+        self.state_now["EmpNow"] = self.state_prev["EmpNow"]
+
+    def get_states(self):                     # AS:1259-1283
+        from . import _lib
+        k = self._hook_const
+        m = torch.empty(self.AgentCount, dtype=torch.float64, device=self.device)
+        k["h"].check(k["h"].lib.aiy_get_states(k["h"].h, _lib.ptr(k["lvl"]), self.AgentCount, float(self.Rnow),
+                                               float(self.Wnow), _lib.ptr(self.state_prev["aNow"]),
+                                               _lib.ptr(self.state_now["LaborSupplyState"]),
+                                               _lib.ptr(self.state_now["EmpNow"]), _lib.ptr(m), _lib.stream_ptr()),
+                     "aiy_get_states")
+        self.state_now["mNow"] = m
+
+    def get_controls(self):                   # AS:1286-1408
+        from . import _lib
+        k = self._hook_const
+        sol = self.solution[0]
+        S, n_M, n1 = sol.m_tab.shape
+        Mg = np.ascontiguousarray(sol.M_grid_host(), dtype=np.float64)
+        c = torch.empty(self.AgentCount, dtype=torch.float64, device=self.device)
+        k["h"].check(k["h"].lib.aiy_get_controls(k["h"].h, S, n_M, n1 - 1, _lib.ptr(sol.m_tab), _lib.ptr(sol.c_tab),
+                                                 Mg.ctypes.data_as(_lib.c_double_p), int(self.shocks["Mrkv"]),
+                                                 float(self.Mnow), self.AgentCount, _lib.ptr(self.state_now["mNow"]),
+                                                 _lib.ptr(self.state_now["LaborSupplyState"]),
+                                                 _lib.ptr(self.state_now["EmpNow"]), _lib.ptr(c), _lib.stream_ptr()),
+                     "aiy_get_controls")
+        self.controls["cNow"] = c
+
+    def get_poststates(self):                 # AS:1411-1415
+        from . import _lib
+        k = self._hook_const
+        a = torch.empty(self.AgentCount, dtype=torch.float64, device=self.device)
+        k["h"].check(k["h"].lib.aiy_get_poststates(k["h"].h, self.AgentCount, _lib.ptr(self.state_now["mNow"]),
+                                                   _lib.ptr(self.controls["cNow"]), _lib.ptr(a), _lib.stream_ptr()),
+                     "aiy_get_poststates")
+        self.state_now["aNow"] = a
 
 
 class AiyagariEconomy:
@@ -293,9 +384,13 @@ class AiyagariEconomy:
 
     def make_history(self):
         """[HARK] Market.make_history: act_T periods of sow -> cultivate -> reap -> mill ->
-        store, fused on device (libaiyagari aiy_sim_periods)."""
+        store.  history_engine "fused" (default): all periods on device in one pass
+        (libaiyagari aiy_sim_periods); "hooks": the period loop on the host calling the
+        market and agent hooks one at a time (aiy_get_shocks .. aiy_sum per period)."""
         if len(self.agents) != 1:
             raise NotImplementedError("the reference economy has exactly one AgentType")
+        if getattr(self, "history_engine", "fused") == "hooks":
+            return self.make_history_hooks()
         agent = self.agents[0]
         self.reset()
         p = agent.panel
@@ -318,6 +413,52 @@ class AiyagariEconomy:
         torch.cuda.synchronize(agent.device)
         self.store_history(agent, p.sow_host(), p.a.cpu().numpy(), p.lab.cpu().numpy(), p.hist_A.cpu().numpy(),
                            p.hist_M.cpu().numpy())
+
+    # ---- [HARK] Market's per-period hooks ----------------------------------------------
+    def make_history_hooks(self):
+        self.reset()
+        for a in self.agents:
+            a.ge_iter = getattr(self, "_ge_iter", 0)
+        for _ in range(self.act_T):
+            self.sow()
+            self.cultivate()
+            self.reap()
+            self.mill()
+            self.store()
+        self.history = {k: np.asarray(v) for k, v in self.history.items()}
+        self.reap_state = {k: [x.cpu().numpy().astype(np.float64) if torch.is_tensor(x) else x for x in v]
+                           for k, v in self.reap_state.items()}
+
+    def sow(self):                           # [HARK] Market.sow
+        for var in self.sow_vars:
+            for a in self.agents:
+                if var in a.shock_vars:
+                    a.shocks[var] = self.sow_state[var]
+                else:
+                    setattr(a, var, self.sow_state[var])
+
+    def cultivate(self):                      # [HARK] Market.cultivate
+        for a in self.agents:
+            a.market_action()
+
+    def reap(self):                           # [HARK] Market.reap
+        for var in self.reap_vars:
+            self.reap_state[var] = [a.state_now[var] for a in self.agents]
+
+    def mill(self):                           # [HARK] Market.mill
+        product = self.mill_rule(**self.reap_state)
+        for i, var in enumerate(self.sow_vars):
+            self.sow_state[var] = product[i]
+
+    def store(self):                          # [HARK] Market.store
+        for var in self.track_vars:
+            if var in self.sow_state:
+                v = self.sow_state[var]
+            elif var in self.reap_state:
+                v = self.reap_state[var]
+            else:
+                v = getattr(self, var)
+            self.history[var].append(v)
 
     def market_constants(self):
         """Constants of calc_R_and_W (AS:1867-1894) for the device mill."""
@@ -372,9 +513,14 @@ class AiyagariEconomy:
 
     def calc_R_and_W(self, aNow, EmpNow):
         """AS:1839-1894 for one period given the agents' assets (scalar formulas; the
-        device path fuses this into aiy_sim_periods)."""
-        Aprev = float(np.mean(np.array(aNow)))
-        Urate = 1.0 - float(np.mean(np.array(EmpNow)))
+        device path fuses this into aiy_sim_periods).  Device-resident harvests (the
+        per-period hooks) are averaged on device (aiy_sum)."""
+        if torch.is_tensor(aNow[0]):
+            Aprev = self._device_mean(aNow)
+            Urate = 1.0 - self._device_mean([e.to(torch.float64) for e in EmpNow])
+        else:
+            Aprev = float(np.mean(np.array(aNow)))
+            Urate = 1.0 - float(np.mean(np.array(EmpNow)))
         self.Urate = Urate
         Mrkv = self.MrkvNow_hist[self.Shk_idx]
         Prod, L = (self.ProdB, (1.0 - self.UrateB) * self.LbrInd) if Mrkv == 0 else \
@@ -385,6 +531,17 @@ class AiyagariEconomy:
         W = Prod * self.Wfunc(k)
         self.KtoLnow = k
         return R * Aprev + W * L, Aprev, Mrkv, R, W
+
+    @staticmethod
+    def _device_mean(xs):
+        """np.mean(np.array(xs)) of device arrays: fixed-order sums (aiy_sum), one
+        host read."""
+        from . import _lib
+        out = torch.empty(len(xs), dtype=torch.float64, device=xs[0].device)
+        h = _lib.handle(xs[0].device.index)
+        for i, x in enumerate(xs):
+            h.check(h.lib.aiy_sum(h.h, _lib.ptr(x), x.numel(), _lib.ptr(out[i:i + 1]), _lib.stream_ptr()), "aiy_sum")
+        return float(out.cpu().numpy().sum()) / sum(x.numel() for x in xs)
 
     def calc_AFunc(self, Mnow, Aprev):
         """AS:1896-1964: per-state OLS of log A_t on log M_{t-1} after T_discard, damped."""

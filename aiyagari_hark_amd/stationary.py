@@ -112,13 +112,18 @@ class StationaryBatch:
         self.mass = torch.empty(shp, dtype=F64, device=dev)
         self.work = torch.empty((2,) + shp, dtype=F64, device=dev)
 
-    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000, warm=False, warm_egm=False):
+    def capital_supply(self, r, egm_tol=1e-8, hist_tol=1e-12, max_hist=200000, warm=False, warm_egm=False,
+                       accel=0):
         """K_s(r) for every calibration (r: array [n_cal]).  warm=True starts the
         distribution iteration from the previous call's stationary mass instead of the
         uniform one (same fixed point, to hist_tol; used between bisection steps, where r
         moves by half the bracket each step).  warm_egm=True starts the household solve
         from the previous call's converged policy (aiy_egm_solve_from): the fixed point
-        moves by ~egm_tol / (1 - beta R), far inside the 1e-5 tolerance on r."""
+        moves by ~egm_tol / (1 - beta R), far inside the 1e-5 tolerance on r.  accel=E > 0
+        lets the device-resident distribution iteration extrapolate along its slowest mode
+        every E iterations (Aitken, AIY_OPT_HIST_ACCEL): the same fixed point to the
+        iteration's own accuracy (~1e-7 relative in K), 1.5-3x fewer
+        iterations; 0 is the oracle's plain iteration."""
         n_cal, S = len(self.cals), self.S
         r = np.asarray(r, dtype=np.float64)
         w, _ = firm_prices(r, self.alpha, self.delta)
@@ -141,9 +146,13 @@ class StationaryBatch:
             self.mass.fill_(1.0 / (S * self.n_a))
         K = (ctypes.c_double * n_cal)()
         iters = (ctypes.c_int32 * n_cal)()
-        h.check(h.lib.aiy_hist_solve(h.h, n_cal, S, self.n_a, _lib.ptr(self.lo), _lib.ptr(self.wlo),
-                                     _lib.ptr(self.d_P), _lib.ptr(self.d_a), float(hist_tol), int(max_hist), 64,
-                                     _lib.ptr(self.mass), _lib.ptr(self.work), K, iters, sp), "aiy_hist_solve")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_ACCEL, int(accel)), "aiy_set_option")
+        try:
+            h.check(h.lib.aiy_hist_solve(h.h, n_cal, S, self.n_a, _lib.ptr(self.lo), _lib.ptr(self.wlo),
+                                         _lib.ptr(self.d_P), _lib.ptr(self.d_a), float(hist_tol), int(max_hist), 64,
+                                         _lib.ptr(self.mass), _lib.ptr(self.work), K, iters, sp), "aiy_hist_solve")
+        finally:
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_ACCEL, 0), "aiy_set_option")
         self.last_tables = (m, c)
         self._mass_valid = True
         return np.array(K[:]), np.array(cycles), np.array(iters[:])
@@ -226,9 +235,37 @@ class _Brent:
         self.x = xcur
 
 
+def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo=None,
+                         r_hi=None):
+    """The whole E1 search in ONE library call (aiy_ge_stationary: the bracket updates run
+    in C++ between device K_s evaluations).  Returns (r, K, Ks, steps, egm_cycles_sum,
+    hist_iters_sum)."""
+    n = len(b.cals)
+    h = _lib.handle(b.device.index)
+    work = torch.empty(int(h.lib.aiy_ge_stationary_work_bytes(n, b.S, b.n_a)), dtype=torch.uint8, device=b.device)
+    host = lambda x: (ctypes.c_double * n)(*[float(v) for v in x])  # noqa: E731
+    alpha, delta = host(b.alpha), host(b.delta)
+    disc = host([c.DiscFac for c in b.cals])
+    model = _lib.StationaryModel(n, b.S, b.n_a, _lib.ptr(b.d_a), _lib.ptr(b.d_P), _lib.ptr(b.d_lab),
+                                 _lib.ptr(b.d_beta), _lib.ptr(b.d_crra), ctypes.addressof(alpha),
+                                 ctypes.addressof(delta), ctypes.addressof(disc))
+    lo = host(np.broadcast_to(np.asarray(r_lo, float), (n,))) if r_lo is not None else None
+    hi = host(np.broadcast_to(np.asarray(r_hi, float), (n,))) if r_hi is not None else None
+    opt = _lib.GeOptions({"bisect": 0, "brent": 1}[method], float(r_tol), float(egm_tol), float(hist_tol),
+                         int(max_steps), 5000, 200000, int(bool(warm_hist)), int(bool(warm_egm)), int(accel),
+                         ctypes.addressof(lo) if lo is not None else None,
+                         ctypes.addressof(hi) if hi is not None else None)
+    r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
+    steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
+                                    ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its), _lib.stream_ptr()),
+            "aiy_ge_stationary")
+    return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value))
+
+
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
-                 method="bisect", warm_egm=None):
+                 method="bisect", warm_egm=None, accel=None, engine="native"):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -238,7 +275,11 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     warm_hist: each step's distribution iteration starts from the previous step's
     stationary mass (the oracle, oracle/stationary.py, starts from uniform; both converge
     to the same distribution to hist_tol).  warm_egm (default: on for "brent"): each
-    step's household solve starts from the previous step's policy."""
+    step's household solve starts from the previous step's policy.  accel (default: 32
+    for "brent", 0 for "bisect"): Aitken period of the distribution iteration
+    (StationaryBatch.capital_supply).
+    engine: "native" -- one aiy_ge_stationary call (C++ search loop); "python" -- the same
+    search driven from Python step by step (per-step logs; identical iterates)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     b = StationaryBatch(cals, aGrid, device=device)
@@ -248,15 +289,24 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         np.broadcast_to(np.asarray(r_hi, float), (n,)).copy()
     if warm_egm is None:
         warm_egm = method == "brent"
+    if accel is None:
+        accel = 32 if method == "brent" else 0
     steps = 0
     cyc_log, it_log = [], []
     Ks = np.zeros(n)
+    if engine == "native" and log is None:
+        r, K, Ks, steps, cyc_sum, it_sum = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
+                                                                warm_hist, warm_egm, accel, r_lo if r_lo is not None
+                                                                else None, r_hi if r_hi is not None else None)
+        KtoY = K ** (1.0 - b.alpha)
+        return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
+                                egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])])
     if method == "brent":
         search = [_Brent(lo[k], hi[k], r_tol) for k in range(n)]
         while not all(sr.done for sr in search) and steps < max_steps:
             x = np.array([sr.propose() for sr in search])
             Ks, cycles, iters = b.capital_supply(x, egm_tol=egm_tol, hist_tol=hist_tol, warm=warm_hist and steps > 0,
-                                                 warm_egm=warm_egm and steps > 0)
+                                                 warm_egm=warm_egm and steps > 0, accel=accel)
             _, Kd = firm_prices(x, b.alpha, b.delta)
             for k, sr in enumerate(search):
                 sr.update(float(Ks[k] - Kd[k]))
@@ -270,7 +320,8 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         while np.any(hi - lo > r_tol) and steps < max_steps:
             mid = 0.5 * (lo + hi)
             Ks, cycles, iters = b.capital_supply(mid, egm_tol=egm_tol, hist_tol=hist_tol,
-                                                 warm=warm_hist and steps > 0, warm_egm=warm_egm and steps > 0)
+                                                 warm=warm_hist and steps > 0, warm_egm=warm_egm and steps > 0,
+                                                 accel=accel)
             _, Kd = firm_prices(mid, b.alpha, b.delta)
             up = Ks > Kd
             hi = np.where(up, mid, hi)

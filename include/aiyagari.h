@@ -218,6 +218,37 @@ int32_t aiy_sim_period_prices(aiy_handle* h, const aiy_panel_model* model, const
                               int64_t n_total, int32_t t, double* sow, double* hist_A, double* hist_M,
                               aiy_stream stream);
 
+/* The reference's per-period simulation hooks one at a time, for a driver that steps
+ * [HARK] Market.make_history period by period (sow -> cultivate -> reap -> mill -> store)
+ * through AgentType.sim_one_period's get_shocks / get_states / get_controls /
+ * get_poststates (AiyagariType, Aiyagari_Support.py:1217-1415).  One small launch each,
+ * all asynchronous on `stream`; the fused aiy_sim_periods computes the same thing per
+ * period in one pass.  All arrays are DEVICE arrays of the n agents unless noted.
+ *   aiy_get_shocks:     lab <- inverse-CDF draw from lab_cdf[lab] (AS:1244-1256):
+ *                       u = n uniforms (device) or NULL -> Philox counter
+ *                       ((ge_iter << 20) | t, (agent_offset + i) / 2) as aiy_sim_periods
+ *   aiy_get_states:     m = Rnow * a_prev + Wnow * lab_level[lab] * emp (AS:1276-1283);
+ *                       emp NULL means everyone employed
+ *   aiy_get_controls:   c = cFunc[4 lab + 2 Mrkv + emp](m, Mnow) on the RAW policy tables
+ *                       m_tab / c_tab [S][n_M][n_a + 1] of aiy_egm_solve (HARK
+ *                       LinearInterpOnInterp1D, AS:1295-1408); M_grid_host: HOST [n_M]
+ *   aiy_get_poststates: a = m - c (AS:1415)
+ *   aiy_sum:            out[0] (device) = sum of x in a fixed order (the mill's
+ *                       np.mean(aNow) numerator, AS:1868) */
+int32_t aiy_get_shocks(aiy_handle* h, int32_t n_lab, const double* lab_cdf, int64_t n, int64_t agent_offset,
+                       uint8_t* lab, const double* u, uint64_t seed, uint32_t ge_iter, int32_t t,
+                       aiy_stream stream);
+int32_t aiy_get_states(aiy_handle* h, const double* lab_level, int64_t n, double Rnow, double Wnow,
+                       const double* a_prev, const uint8_t* lab, const uint8_t* emp, double* m_out,
+                       aiy_stream stream);
+int32_t aiy_get_controls(aiy_handle* h, int32_t S, int32_t n_M, int32_t n_a, const double* m_tab,
+                         const double* c_tab, const double* M_grid_host, int32_t Mrkv, double Mnow, int64_t n,
+                         const double* m, const uint8_t* lab, const uint8_t* emp, double* c_out,
+                         aiy_stream stream);
+int32_t aiy_get_poststates(aiy_handle* h, int64_t n, const double* m, const double* c, double* a_out,
+                           aiy_stream stream);
+int32_t aiy_sum(aiy_handle* h, const double* x, int64_t n, double* out, aiy_stream stream);
+
 /* Measurement hook (bench.py): n_launch periods of the panel kernel (single rank,
  * Philox shocks) -- n_launch per-period launches, each bracketed by its own pair of HIP
  * events on `stream`, or with AIY_OPT_RESIDENT one persistent launch of n_launch periods
@@ -289,6 +320,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     per calibration, in-kernel barriers); 0: the push/mix launch pair */
 #define AIY_OPT_HIST_CLUSTER 7   /* maximum workgroups per calibration cluster of the resident
                                     histogram (0: default 32; the minimum the grid size needs wins) */
+#define AIY_OPT_HIST_ACCEL 8     /* value E > 0: the resident histogram extrapolates every E iterations
+                                    along the last change when two consecutive estimates of its
+                                    contraction ratio agree (Aitken; same fixed point, fewer
+                                    iterations, counts differ from the plain iteration); 0 (default):
+                                    the plain iteration of oracle/stationary.py */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
@@ -317,6 +353,51 @@ int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, con
                        const double* wlo, const double* P, const double* a_grid, double tol,
                        int32_t max_iter, int32_t chunk, double* mass, double* work, double* K_out,
                        int32_t* iters_out, aiy_stream stream);
+
+/* ------------- stationary general equilibrium (E1 over E2, SURVEY §8b aiy_ge_bisect) ------------- */
+
+/* A batch of stationary Aiyagari households: the EGM inputs of aiy_egm_solve with one
+ * aggregate node (device arrays) and the firm of calc_R_and_W (AS:1886-1890, L = 1). */
+typedef struct {
+  int32_t n_cal, S, n_a;
+  const double* a_grid;  /* [n_cal][n_a]  device                                  */
+  const double* P;       /* [n_cal][S][S] device: income Markov chain               */
+  const double* lab;     /* [n_cal][S]    device: labour levels (simple-mean norm.) */
+  const double* beta;    /* [n_cal]       device: DiscFac                           */
+  const double* crra;    /* [n_cal]       device: CRRA                              */
+  const double* alpha;   /* [n_cal]       HOST: CapShare                            */
+  const double* delta;   /* [n_cal]       HOST: DeprFac                             */
+  const double* disc;    /* [n_cal]       HOST: DiscFac (bracket end 1 / beta - 1)  */
+} aiy_stationary_model;
+
+typedef struct {
+  int32_t method;        /* 0: bisection on K_s(r) - K_d(r) (oracle ge_bisect); 1: bisection to a
+                            sign change, then Brent's method (scipy brentq) per calibration     */
+  double r_tol;          /* bracket width (bisection) / xtol (Brent)                          */
+  double egm_tol;        /* household solve tolerance (sup-norm of the tables)                */
+  double hist_tol;       /* distribution iteration tolerance (sup-norm of the mass)           */
+  int32_t max_steps, max_egm_cycles, max_hist_iter;
+  int32_t warm_hist;     /* != 0: each step's distribution starts from the previous step's     */
+  int32_t warm_egm;      /* != 0: each step's household solve starts from the previous policy */
+  int32_t accel;         /* Aitken period of the distribution iteration (0: plain)            */
+  const double* r_lo;    /* HOST [n_cal] or NULL: -delta / 2                                   */
+  const double* r_hi;    /* HOST [n_cal] or NULL: 1 / beta - 1 - 1e-9                          */
+} aiy_ge_options;
+
+/* Device scratch the call needs (caller-owned `work`), -1 for bad sizes. */
+int64_t aiy_ge_stationary_work_bytes(int32_t n_cal, int32_t S, int32_t n_a);
+
+/* General equilibrium in r of every calibration (build-defined E1; no reference code):
+ * per step, K_s(r) = sum(mass * a) of the stationary distribution (aiy_egm_solve ->
+ * aiy_hist_lottery -> aiy_hist_solve) against K_d(r) = (alpha / (r + delta))^(1/(1-alpha)),
+ * w(r) = (1 - alpha) K_d^alpha, R = 1 + r; the brackets move on the host.
+ *   r_out, K_out (= K_d(r)), Ks_out (last K_s, may be NULL): HOST [n_cal];
+ *   steps_out: K_s evaluations; egm_cycles_out / hist_iters_out: their sums over steps and
+ *   calibrations (may be NULL).  The converged tables, lottery and mass stay in `work`.
+ * BLOCKING. */
+int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* model, const aiy_ge_options* opt,
+                          void* work, double* r_out, double* K_out, double* Ks_out, int32_t* steps_out,
+                          int32_t* egm_cycles_out, int32_t* hist_iters_out, aiy_stream stream);
 
 /* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
  * the device-resident distribution-iteration launches since the last reset (HIP events on

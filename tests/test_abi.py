@@ -27,7 +27,8 @@ def test_header_lists_expected_entry_points():
     fns = header_functions()
     for must in ("aiy_create", "aiy_destroy", "aiy_egm_step", "aiy_egm_solve", "aiy_sim_periods",
                  "aiy_hist_lottery", "aiy_hist_solve", "aiy_comm_init", "aiy_allreduce_sum", "aiy_policy_eval",
-                 "aiy_wealth_stats", "aiy_sim_period_local", "aiy_sim_period_prices"):
+                 "aiy_wealth_stats", "aiy_sim_period_local", "aiy_sim_period_prices", "aiy_get_shocks",
+                 "aiy_get_states", "aiy_get_controls", "aiy_get_poststates", "aiy_sum", "aiy_ge_stationary"):
         assert must in fns
 
 
@@ -68,6 +69,9 @@ def test_argument_validation_without_gpu(lib):
     assert lib.aiy_create(0, None) == -1
     assert lib.aiy_comm_unique_id(None) == -1
     assert lib.aiy_destroy(None) == 0
+    assert lib.aiy_get_shocks(None, 7, None, 10, 0, None, None, 0, 0, 0, None) == -1
+    assert lib.aiy_get_poststates(None, 10, None, None, None, None) == -1
+    assert lib.aiy_sum(None, None, 10, None, None) == -1
     assert lib.aiy_last_error(None) == b"null handle"
 
 

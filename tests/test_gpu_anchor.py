@@ -1,0 +1,53 @@
+"""Statistical anchor against the reference's own recorded outputs.
+
+The reference holds no tests or fixtures and HARK is not installable here, so the
+oracle's restatement of HARK is "parity unpinned" (DESIGN.md §2).  The one piece of
+reference-held evidence is the notebook's recorded run (Aiyagari-HARK.ipynb cells 16-24:
+rho = 0.3, sigma = 0.2, CRRA = 1, 350 agents, act_T = 11 000, 32-point grid, market
+tolerance 0.01, unseeded global NumPy RNG):
+
+    r = 4.17796158865138 %, saving rate = 23.64927807527217 %      (ipynb:383-384)
+    wealth mean 5.4389159200973145, std 3.69719975669068 (population),
+    median 4.718135905539691, max 22.04633324604029                 (ipynb:525-529)
+
+Its shocks are unseeded, so the run is one draw from a distribution.  Here the SAME
+configuration is solved to its Krusell-Smith fixed point on device for many independent
+shock streams (Philox seeds) in one EconomyBatch, and every recorded statistic must lie
+inside the seed distribution (within 3 standard deviations of its mean).  This pins the
+model -- calibration, discretisation, EGM, panel, GE loop -- to the reference's behaviour;
+it does not pin the arithmetic (that is the oracle parity tests' job)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NOTEBOOK = dict(r=4.17796158865138, s=23.64927807527217, mean=5.4389159200973145, std=3.69719975669068,
+                median=4.718135905539691, max=22.04633324604029)
+
+
+def seed_distribution(gpu, n_seeds=48):
+    from aiyagari_hark_amd.sweep import EconomyBatch, build_economies
+    cell = dict(LaborAR=0.3, LaborSD=0.2, CRRA=1.0)
+    econs = build_economies([cell] * n_seeds, dict(act_T=11000, T_discard=1000), dict(AgentCount=350), device=gpu,
+                            shock_mode="philox", seed0=1000)
+    EconomyBatch(econs).solve()
+    out = {k: [] for k in NOTEBOOK}
+    for e in econs:
+        w = np.asarray(e.reap_state["aNow"][0])
+        K = float(np.mean(w))
+        out["r"].append(100 * (e.sow_state["Rnow"] - 1.0))
+        out["s"].append(100 * 0.08 * K / (e.sow_state["Mnow"] - 0.92 * K))
+        out["mean"].append(K)
+        out["std"].append(float(w.std()))
+        out["median"].append(float(np.median(w)))
+        out["max"].append(float(w.max()))
+    return {k: np.array(v) for k, v in out.items()}
+
+
+@pytest.mark.timeout(300)
+def test_notebook_outputs_inside_seed_distribution(gpu):
+    dist = seed_distribution(gpu)
+    for k, want in NOTEBOOK.items():
+        mu, sd = float(np.mean(dist[k])), float(np.std(dist[k], ddof=1))
+        assert sd > 0, k
+        assert abs(want - mu) <= 3 * sd, (k, want, mu, sd)

@@ -616,3 +616,17 @@ def test_stationary_brent_warm_matches_oracle_bisection(gpu):
         assert abs(res.r[k] - want["r"]) < 2e-7, (k, res.r[k], want["r"])
         assert abs(res.KtoY[k] - want["KtoY"]) < 1e-5
     assert res.bisection_steps < want["iters"]
+
+
+@pytest.mark.parametrize("method", ["bisect", "brent"])
+def test_native_ge_search_equals_python_loop(gpu, method):
+    """aiy_ge_stationary (the E1 search loop in C++) takes exactly the steps of
+    the Python-driven loop: identical r (bit for bit) and step count."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0),
+            Calibration(LaborAR=0.3, LaborSD=0.4, CRRA=3.0)]
+    nat = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="native")
+    py = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="python")
+    assert nat.bisection_steps == py.bisection_steps
+    assert np.array_equal(nat.r, py.r)
+    assert np.array_equal(nat.KtoY, py.KtoY)

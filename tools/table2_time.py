@@ -26,7 +26,7 @@ def main():
     for v in variants:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_RESIDENT, v.get("resident", 1)), "opt")
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, v.get("cluster", 0)), "opt")
-        kw = {k: v[k] for k in ("method", "warm_egm") if k in v}
+        kw = {k: v[k] for k in ("method", "warm_egm", "accel") if k in v}
         ms, n = ctypes.c_double(), ctypes.c_int64()
         h.check(h.lib.aiy_hist_launch_stats(h.h, None, None, 1), "stats")
         torch.cuda.synchronize()
