@@ -12,8 +12,9 @@
 //     with LDS f64 atomics into a per-row destination SPAN buffer: a monotone lottery maps
 //     the contiguous source range to the contiguous destination range
 //     [lo(j0), lo(j1 - 1) + 1] of each row;
-//   * the spans are published write-through (sc1) as the workgroup's slab; one cluster
-//     barrier (agent-scope counter, sc1 polls);
+//   * the parts of the spans outside the own columns are published write-through (sc1) as
+//     the workgroup's slab (the own part stays in LDS); one cluster barrier (agent-scope
+//     counter, sc1 polls);
 //   * gather (destinations = own columns): T_s[d] = sum of the slabs whose span covers d
 //     (the covering workgroups are fixed for the whole solve and found once at start), in
 //     ascending workgroup order, every load of a row group issued before the first use;
@@ -21,8 +22,9 @@
 //     to one published value per workgroup, read by the cluster after the NEXT barrier:
 //     the solve stops exactly where oracle/stationary.py stationary_hist stops (first
 //     iteration with max |mass' - mass| < tol) and keeps that iteration's mass.
-// Per iteration and point: lo 4 B + w 8 B (L2-resident re-reads), slab 8 B out + 8 B in
-// (L2 / MALL), no HBM round trip of the mass, no global atomics, one barrier.
+// Per iteration: the mass and (S <= 8) the lottery stay in registers, only the span
+// entries that cross a workgroup boundary go through memory (write-through slab, MALL),
+// no global atomics, one barrier.
 // Shapes that do not fit (spans beyond the LDS budget, more covering workgroups per row
 // than kHcCand, a non-monotone lottery) abort before the first iteration and the host
 // runs the push/mix pair instead.
@@ -30,6 +32,7 @@
 #include "internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace aiy {
 
@@ -52,7 +55,7 @@ struct HcRun {
   const double* P;        // [n_cal][S][S]
   double* mass;           // [n_cal][S][n_a] in: start, out: final
   double* slab;           // [launch cals][G][2][cap]
-  int* span;              // [launch cals][G][SMAX][2] (first, len)
+  int* span;              // [launch cals][G][SMAX][4] (first, len, left base, right base)
   unsigned* ctr;          // [launch cals][kHcCtrStride]
   double* dist;           // [launch cals][2][G][4]: sup-norm change, Aitken dot products, valid
   double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0)
@@ -64,7 +67,7 @@ struct HcRun {
 };
 
 struct HcCand {
-  int w, first, len, off;
+  int w, first, len, base;   // destination d of the covering span sits at slab/LDS index base + d
 };
 
 // Cluster barrier: lane 0 adds one to the cluster counter (after the caller's drained sc1
@@ -104,6 +107,23 @@ __device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsign
   } while (0)
 #endif
 
+// One covering span's value at destination d: the own span from LDS (read once by the
+// column's owner, then re-zeroed for the next push), a foreign one from its published slab.
+__device__ __forceinline__ double hc_take(const HcCand& c, int w, int d, int par, int cap, const double* slab_cl,
+                                          double* Tacc) {
+  const int q = c.base + d;
+  // two destinations (added at the use): one shared register would make the LDS read
+  // wait for every earlier slab load in flight (write-after-write on the register)
+  double vg = 0.0, vl = 0.0;
+  if (c.w == w) {
+    vl = Tacc[q];
+    Tacc[q] = 0.0;
+  } else {
+    vg = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + q]);
+  }
+  return vg + vl;
+}
+
 // Sum over the 64 lanes (DPP: row shifts, then row broadcasts), valid in lane 63.
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_add_src(double v) {
@@ -122,19 +142,57 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
   return v;
 }
 
+// Cluster barrier of iteration `it` that also counts the workgroups whose last change was
+// not below tol: lane 0 adds (1 | flag << 32) to the 64-bit word of the iteration's parity
+// (low half: arrivals, high half: cumulative flags of that parity; a workgroup can run at
+// most one barrier ahead, so the other parity's word takes its early add) and waits for
+// G * (barriers of this parity so far) arrivals.  *nc_out: the flag count of this parity
+// after every workgroup's add.  False on timeout (error word set).
+__device__ __forceinline__ bool hc_barrier_count(const HcRun& r, unsigned long long* cw, unsigned target,
+                                                 unsigned flag, unsigned* nc_out, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long v = __hip_atomic_fetch_add(cw, 1ull | ((unsigned long long)flag << 32), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) +
+                           (1ull | ((unsigned long long)flag << 32));
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while ((unsigned)v < target) {
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+        __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *nc_out = (unsigned)(v >> 32);
+    *s_flag = ok;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 template <int SMAX, int KC, int TH>
 __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 #ifdef AIY_DIAG_PHASES
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = 0;
 #endif
-  extern __shared__ double Tacc[];                 // destination spans of this workgroup
-  __shared__ int s_first[SMAX], s_off[SMAX + 1];
+  // Span buffer (LDS Tacc and the published slab alike): row after row, destination d of
+  // row s at s_base[s] + d.  Only the parts outside the own columns are published
+  // (s_pub: per row the ranges below j0 and from j1 on).
+  extern __shared__ double Tacc[];
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
   __shared__ HcCand s_cand[SMAX][kHcCand];
   __shared__ int s_ncand[SMAX];
   __shared__ double s_red[TH / kWave];
   __shared__ int s_cinfo[KC * SMAX * TH];
   __shared__ int s_flag, s_stop;
-  __shared__ double s_dot[2][TH / kWave];
+  __shared__ unsigned s_nc;
+  __shared__ double s_dot[2];
+  __shared__ double s_dotw[2][TH / kWave];
   __shared__ double s_lam[2], s_fext;
   __shared__ double s_P[SMAX * SMAX];              // P[s][s'] zero-padded to SMAX x SMAX
 
@@ -146,6 +204,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
   const int j0 = w * r.nj;
   const int j1 = min(j0 + r.nj, n_a);
   unsigned* ctr = r.ctr + (size_t)lc * kHcCtrStride;
+  unsigned long long* cw = reinterpret_cast<unsigned long long*>(ctr + 2);   // [2] per-parity words
   double* dist = r.dist + (size_t)lc * 2 * G * 4;
   double* DB = r.dbuf ? r.dbuf + (size_t)cal * S * n_a : nullptr;
   const int E = r.accel;
@@ -155,9 +214,9 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
   double* MS = r.mass + row0 * n_a;
   double* slab_cl = r.slab + (size_t)lc * G * 2 * cap;
   const double* __restrict__ Pc = r.P + (size_t)cal * S * S;
-  int* span_cl = r.span + (size_t)lc * G * SMAX * 2;
+  int* span_cl = r.span + (size_t)lc * G * SMAX * 4;   // per (w, s): first, len, base
 
-  // ---- setup: P, own spans, mass -> registers ----
+  // ---- setup: P, own spans and their layout, mass -> registers ----
   for (int q = tid; q < SMAX * SMAX; q += TH) {
     const int s = q / SMAX, sp = q - s * SMAX;
     s_P[q] = (s < S && sp < S) ? Pc[s * S + sp] : 0.0;
@@ -168,14 +227,21 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     for (int s = 0; s < S; ++s) {
       const int f = LO[(size_t)s * n_a + j0];
       const int l = LO[(size_t)s * n_a + j1 - 1] - f + 2;   // destinations lo .. lo_last + 1
-      s_first[s] = f;
-      s_off[s] = tot;
       if (l < 2 || f < 0 || f + l > n_a) bad = 2u;          // not a monotone lottery of ours
-      tot += l > 0 ? l : 0;
-      __hip_atomic_store(&span_cl[((size_t)w * SMAX + s) * 2], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&span_cl[((size_t)w * SMAX + s) * 2 + 1], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int ll = l > 0 ? l : 0;
+      s_base[s] = tot - f;
+      // foreign parts of the row: destinations below j0 and from j1 on
+      s_pub[2 * s][0] = tot;
+      s_pub[2 * s][1] = tot + max(0, min(ll, j0 - f));
+      s_pub[2 * s + 1][0] = tot + min(ll, max(0, j1 - f));
+      s_pub[2 * s + 1][1] = tot + ll;
+      int* sp = &span_cl[((size_t)w * SMAX + s) * 4];
+      __hip_atomic_store(&sp[0], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[1], ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[2], tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot += ll;
     }
-    s_off[S] = tot;
+    s_tot = tot;
     if (tot > cap) bad = 2u;
     if (bad) __hip_atomic_store(r.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -196,13 +262,12 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     const int s = tid;
     int n = 0, bad = 0;
     for (int w2 = 0; w2 < G; ++w2) {
-      int off = 0;
-      for (int s2 = 0; s2 < s; ++s2)
-        off += __hip_atomic_load(&span_cl[((size_t)w2 * SMAX + s2) * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int f = __hip_atomic_load(&span_cl[((size_t)w2 * SMAX + s) * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int l = __hip_atomic_load(&span_cl[((size_t)w2 * SMAX + s) * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int* sp = &span_cl[((size_t)w2 * SMAX + s) * 4];
+      const int f = __hip_atomic_load(&sp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int l = __hip_atomic_load(&sp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (f < j1 && f + l > j0) {
-        if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, off};
+        const int base = __hip_atomic_load(&sp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, base};
         else bad = 1;
         ++n;
       }
@@ -213,7 +278,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
-  const int total = s_off[S];
+  const int total = s_tot;
   for (int q = tid; q < total; q += TH) Tacc[q] = 0.0;
   if (!hc_barrier(r, ctr, 2u * G, &s_flag)) return;
   if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
@@ -243,7 +308,8 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 
   const int lane = tid & (kWave - 1);
   double dloc = 0.0;   // this workgroup's sup-norm change of the last mix
-  double aloc = 0.0, bloc = 0.0, vloc = 0.0;   // Aitken dot products of the last mix, valid flag
+  double aloc = 0.0, bloc = 0.0;   // Aitken dot products of the last mix
+  unsigned nc_prev[2] = {0u, 0u};  // thread 0: flag counts of the two parities
   int final_it = 0;
   if (tid == 0) {
     s_lam[0] = s_lam[1] = -1.0;
@@ -266,6 +332,15 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       }
     }
   }
+  // per-row span bases (lane s) and publish ranges (lane r: [lo, hi)) held in VGPR lanes,
+  // read with v_readlane inside the loop (no LDS round trip per row)
+  const int v_base = lane < S ? s_base[lane] : 0;
+  const int v_plo = lane < 2 * S ? s_pub[lane][0] : 0;
+  const int v_phi = lane < 2 * S ? s_pub[lane][1] : 0;
+  // Aitken phases of mix `it` (it % E): E - 2 store the difference; E - 1 and 0 form the
+  // dot products <d_it, d_it-1>, |d_it-1|^2 of two consecutive ratio estimates; at 1 the
+  // cluster may extrapolate along d_it (s_fext, decided from those two estimates)
+  auto is_dot = [&](int i) { return E > 0 && i >= E - 1 && (i % E == E - 1 || i % E == 0); };
   for (int it = 1; it <= r.max_iter; ++it) {
     const int par = it & 1;
     HC_PH(0);
@@ -306,17 +381,17 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
               const int d = dd[k][q];
               const double vlo = ww[k][q] * m[k][s];            // np.add.at(T[s], lo, wlo * mass)
               const double vhi = (1.0 - ww[k][q]) * m[k][s];    // np.add.at(T[s], lo + 1, (1 - wlo) * mass)
-              const int base = s_off[s] - s_first[s];
+              const int ilo = __builtin_amdgcn_readlane(v_base, s) + d, ihi = ilo + 1;
               const int d0 = __builtin_amdgcn_readfirstlane(d);
               if (__all(act && d == d0)) {
                 const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
                 if (lane == kWave - 1) {
-                  atomicAdd(&Tacc[base + d0], tl);
-                  if (th != 0.0) atomicAdd(&Tacc[base + d0 + 1], th);
+                  atomicAdd(&Tacc[ilo], tl);
+                  if (th != 0.0) atomicAdd(&Tacc[ihi], th);
                 }
               } else if (act) {
-                if (vlo != 0.0) atomicAdd(&Tacc[base + d], vlo);
-                if (vhi != 0.0) atomicAdd(&Tacc[base + d + 1], vhi);
+                if (vlo != 0.0) atomicAdd(&Tacc[ilo], vlo);
+                if (vhi != 0.0) atomicAdd(&Tacc[ihi], vhi);
               }
             }
           }
@@ -325,25 +400,31 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     }
     __syncthreads();
     HC_PH(1);
-    // ---- publish the spans write-through, re-zero the buffer ----
+    // ---- publish the parts of the spans outside the own columns write-through and re-zero
+    // them; the own part stays in LDS for the own gather ----
     double* slab = slab_cl + ((size_t)w * 2 + par) * cap;
-    for (int q = tid; q < total; q += TH) {
-      store_f64_agent(&slab[q], Tacc[q]);
-      Tacc[q] = 0.0;
+    for (int rr = 0; rr < 2 * S; ++rr) {
+      const int lo = __builtin_amdgcn_readlane(v_plo, rr), hi = __builtin_amdgcn_readlane(v_phi, rr);
+      for (int q = lo + tid; q < hi; q += TH) {
+        store_f64_agent(&slab[q], Tacc[q]);
+        Tacc[q] = 0.0;
+      }
     }
-    if (tid == 0) {   // the previous mix's change (iteration it - 1) and its Aitken products
+    const bool dot_prev = is_dot(it - 1);   // mix it - 1 formed Aitken dot products
+    if (tid == 0 && dot_prev) {
       double* dp = &dist[((size_t)((it - 1) & 1) * G + w) * 4];
-      store_f64_agent(&dp[0], dloc);
       store_f64_agent(&dp[1], aloc);
       store_f64_agent(&dp[2], bloc);
-      store_f64_agent(&dp[3], vloc);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     HC_PH(2);
-    if (!hc_barrier(r, ctr, (unsigned)(it + 2) * G, &s_flag)) return;
+    // the barrier carries the stop test: flag = change of mix it - 1 not below tol (NaN
+    // included, as np.max(...) < tol is False for NaN)
+    const unsigned flag = (it >= 2 && dloc < r.tol) ? 0u : 1u;
+    if (!hc_barrier_count(r, &cw[par], (unsigned)G * (unsigned)((it + par) / 2), flag, &s_nc, &s_flag)) return;
     HC_PH(3);
-    // ---- gather own destinations from the covering slabs (ascending w); the stop check
-    // runs while the first row group's loads are in flight ----
+    // ---- gather own destinations from the covering spans (ascending w): foreign ones from
+    // their slabs, the own one from LDS ----
     constexpr int GR = HcGather<SMAX, KC, TH>::kRows;
     double T[KC][SMAX];
 #pragma unroll
@@ -355,6 +436,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     for (int s0 = 0; s0 < SMAX; s0 += GR) {
       if (s0 < S) {
         double v0[KC][GR], v1[KC][GR];
+        int oq[KC][GR];   // LDS index of the own span's share, -1: none among the first two
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
           const int d = j0 + tid + k * TH;
@@ -363,78 +445,77 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
             const int s = s0 + q;
             v0[k][q] = 0.0;
             v1[k][q] = 0.0;
+            oq[k][q] = -1;
             if (s < S) {
               const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
               if (cn >= 1) {
-                const HcCand c0 = s_cand[s][cf];
-                v0[k][q] = load_f64_agent(&slab_cl[((size_t)c0.w * 2 + par) * cap + c0.off + d - c0.first]);
+                const HcCand c = s_cand[s][cf];
+                if (c.w != w) v0[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
               }
               if (cn >= 2) {
-                const HcCand c1 = s_cand[s][cf + 1];
-                v1[k][q] = load_f64_agent(&slab_cl[((size_t)c1.w * 2 + par) * cap + c1.off + d - c1.first]);
+                const HcCand c = s_cand[s][cf + 1];
+                if (c.w != w) v1[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
               }
               more = more || cn > 2;
             }
           }
         }
-        if (s0 == 0 && it >= 2) {
-          // stop where the oracle stops: max change of iteration it - 1 < tol
-          if (tid < kWave) {
-            // every workgroup's (change, dot products, valid) of mix it - 1: all loads of
-            // the wave in flight together (kHcMaxG <= 2 * 64 workgroups)
-            const double* dq = &dist[(size_t)((it - 1) & 1) * G * 4];
-            double xd[2], xa[2], xb[2], xv[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int w2 = lane + u * kWave;
-              const bool ok = w2 < G;
-              xd[u] = ok ? load_f64_agent(&dq[w2 * 4 + 0]) : 0.0;
-              xa[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 1]) : 0.0;
-              xb[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 2]) : 0.0;
-              xv[u] = ok && E > 0 ? load_f64_agent(&dq[w2 * 4 + 3]) : 0.0;
-            }
-            const double dd2 = wave_nan_max(nan_max(xd[0], xd[1]));
-            // fixed-order sums over the workgroups (lane pairs, then the DPP tree)
-            const double asum = wave_sum_lane63(xa[0] + xa[1]);
-            const double bsum = wave_sum_lane63(xb[0] + xb[1]);
-            const double valid = xv[0];
-            if (lane == kWave - 1) {
-              s_dot[0][0] = asum;
-              s_dot[1][0] = bsum;
-            }
-            if (tid == 0) {
-              s_stop = (dd2 < r.tol) ? 1 : 0;
-              s_red[0] = valid;
-            }
-          }
-          __syncthreads();
-          if (tid == 0) {
-            {
-              // Aitken: the cluster's dot products of mix it - 1
-              if (E > 0 && s_red[0] != 0.0) {
-                const double a = s_dot[0][0], b = s_dot[1][0];
-                const int ph = (it - 1) % E;           // E - 1: first estimate, 0: second
-                s_lam[ph == 0 ? 1 : 0] = b > 0.0 ? a / b : -1.0;
-              }
-              s_fext = 0.0;
-              if (E > 0 && it > E && it % E == 1) {
-                const double l0 = s_lam[0], l1 = s_lam[1];
-                if (l1 > 0.5 && l1 < 1.0 - 1e-9 && fabs(l1 - l0) < 1e-3 * (1.0 - l1)) s_fext = l1 / (1.0 - l1);
-                s_lam[0] = s_lam[1] = -1.0;
-              }
-            }
-          }
-          __syncthreads();
-        }
+        // the own span's share once every slab load of the group is in flight (with two
+        // covering spans the sum does not depend on their order)
 #pragma unroll
         for (int k = 0; k < KC; ++k)
 #pragma unroll
-          for (int q = 0; q < GR; ++q) T[k][s0 + q] = v0[k][q] + v1[k][q];
+          for (int q = 0; q < GR; ++q)
+            if (oq[k][q] >= 0) {
+              T[k][s0 + q] = Tacc[oq[k][q]];
+              Tacc[oq[k][q]] = 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int q = 0; q < GR; ++q) T[k][s0 + q] = (v0[k][q] + v1[k][q]) + T[k][s0 + q];
       }
     }
-    if (it >= 2 && s_stop) {
+    // stop where the oracle stops: the first iteration whose max change is < tol, keeping
+    // that iteration's mass (no flag of this barrier's parity was added)
+    if (it >= 2 && s_nc == nc_prev[par]) {
       final_it = it - 1;
       break;
+    }
+    nc_prev[par] = s_nc;
+    if (dot_prev) {   // Aitken: the cluster's dot products of mix it - 1
+      if (tid < kWave) {
+        const double* dq = &dist[(size_t)((it - 1) & 1) * G * 4];
+        double xa[2], xb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int w2 = lane + u * kWave;
+          const bool ok = w2 < G;
+          xa[u] = ok ? load_f64_agent(&dq[w2 * 4 + 1]) : 0.0;
+          xb[u] = ok ? load_f64_agent(&dq[w2 * 4 + 2]) : 0.0;
+        }
+        // fixed-order sums over the workgroups (lane pairs, then the DPP tree)
+        const double asum = wave_sum_lane63(xa[0] + xa[1]);
+        const double bsum = wave_sum_lane63(xb[0] + xb[1]);
+        if (lane == kWave - 1) {
+          s_dot[0] = asum;
+          s_dot[1] = bsum;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        const double a = s_dot[0], b = s_dot[1];
+        const int ph = (it - 1) % E;           // E - 1: first estimate, 0: second
+        s_lam[ph == 0 ? 1 : 0] = b > 0.0 ? a / b : -1.0;
+        if (it > E && it % E == 1) {
+          const double l0 = s_lam[0], l1 = s_lam[1];
+          if (l1 > 0.5 && l1 < 1.0 - 1e-9 && fabs(l1 - l0) < 1e-3 * (1.0 - l1)) s_fext = l1 / (1.0 - l1);
+          s_lam[0] = s_lam[1] = -1.0;
+        }
+      }
+      __syncthreads();
     }
     HC_PH(4);
     if (__any(more)) {   // columns covered by > 2 spans (the borrowing constraint)
@@ -451,10 +532,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
               for (int u = 0; u < 4; ++u) {
                 const int c = c0 + u;
                 x[u] = 0.0;
-                if (c < cn) {
-                  const HcCand cx = s_cand[s][cf + c];
-                  x[u] = load_f64_agent(&slab_cl[((size_t)cx.w * 2 + par) * cap + cx.off + d - cx.first]);
-                }
+                if (c < cn) x[u] = hc_take(s_cand[s][cf + c], w, d, par, cap, slab_cl, Tacc);
               }
               T[k][s] += ((x[0] + x[1]) + x[2]) + x[3];
             }
@@ -463,38 +541,52 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       }
     }
     HC_PH(5);
-    // Aitken phases of this mix (it % E): E - 2 store the difference; E - 1 and 0 form the
-    // dot products <d_it, d_it-1>, |d_it-1|^2 of two consecutive ratio estimates; at 1 the
-    // cluster may extrapolate along d_it (s_fext, decided above from those two estimates)
     const int aph = E > 0 ? it % E : -1;
     const bool a_store = E > 0 && (aph == E - 2 || aph == E - 1);
-    const bool a_dot = E > 0 && it >= E - 1 && (aph == E - 1 || aph == 0);
+    const bool a_dot = is_dot(it);
     const double fext = s_fext;
     double dmax = 0.0, ap = 0.0, bp = 0.0;
+    // branch-free over the padded SMAX x SMAX block (rows and columns beyond S and the
+    // columns beyond j1 carry zeros), one column of P in registers at a time (the next
+    // one's LDS reads in flight; the empty asm keeps the compiler from hoisting all of P
+    // into registers), the Aitken bookkeeping (2-3 of every E iterations) in its own copy
+    auto mix = [&](auto aitken) {
+      double pc[SMAX], pn[SMAX];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      const int j = j0 + tid + k * TH;
-      const bool act = j < j1;
+      for (int s = 0; s < SMAX; ++s) pc[s] = s_P[s * SMAX];
 #pragma unroll
       for (int sp = 0; sp < SMAX; ++sp) {
-        if (sp < S) {
+        if (sp + 1 < SMAX) {
+#pragma unroll
+          for (int s = 0; s < SMAX; ++s) pn[s] = s_P[s * SMAX + sp + 1];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int j = j0 + tid + k * TH;
           double acc = 0.0;
 #pragma unroll
-          for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * T[k][s];   // P.T @ T (LDS broadcast; T = 0 beyond S)
+          for (int s = 0; s < SMAX; ++s) acc += pc[s] * T[k][s];   // P.T @ T
           const double dnew = acc - m[k][sp];
-          if (act) {
-            dmax = nan_max(dmax, fabs(dnew));
-            if (a_dot) {   // 2 of every E iterations: the load latency does not matter
-              const double dprev = DB[(size_t)sp * n_a + j];
-              ap += dnew * dprev;
-              bp += dprev * dprev;
+          dmax = nan_max(dmax, fabs(dnew));
+          if constexpr (decltype(aitken)::value) {
+            if (j < j1 && sp < S) {
+              if (a_dot) {
+                const double dprev = DB[(size_t)sp * n_a + j];
+                ap += dnew * dprev;
+                bp += dprev * dprev;
+              }
+              if (a_store) DB[(size_t)sp * n_a + j] = dnew;
             }
-            if (a_store) DB[(size_t)sp * n_a + j] = dnew;
           }
-          m[k][sp] = fext != 0.0 ? acc + fext * dnew : acc;   // x* ~ x + d lambda / (1 - lambda)
+          m[k][sp] = acc + fext * dnew;   // fext = 0: acc; else x* ~ x + d lambda / (1 - lambda)
         }
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) pc[s] = pn[s];
       }
-    }
+    };
+    if (a_dot || a_store) mix(std::true_type{});
+    else mix(std::false_type{});
     HC_PH(6);
     dmax = wave_nan_max(dmax);
     if (lane == 0) s_red[tid / kWave] = dmax;
@@ -502,8 +594,8 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       ap = wave_sum_lane63(ap);
       bp = wave_sum_lane63(bp);
       if (lane == kWave - 1) {
-        s_dot[0][tid / kWave] = ap;
-        s_dot[1][tid / kWave] = bp;
+        s_dotw[0][tid / kWave] = ap;
+        s_dotw[1][tid / kWave] = bp;
       }
     }
     __syncthreads();
@@ -512,19 +604,19 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       for (int q = 1; q < TH / kWave; ++q) d = nan_max(d, s_red[q]);
       dloc = d;
       aloc = bloc = 0.0;
-      vloc = a_dot ? 1.0 : 0.0;
       if (a_dot)
         for (int q = 0; q < TH / kWave; ++q) {
-          aloc += s_dot[0][q];
-          bloc += s_dot[1][q];
+          aloc += s_dotw[0][q];
+          bloc += s_dotw[1][q];
         }
+      s_fext = 0.0;
     }
     HC_PH(7);
     final_it = it;
   }
 #ifdef AIY_DIAG_PHASES
   if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES && final_it > 0)
-    printf("[hist phases] block %d G=%d nj=%d iters=%d us/iter: push %.2f publish %.2f barrier %.2f check+gather %.2f "
+    printf("[hist phases] block %d G=%d nj=%d iters=%d us/iter: push %.2f publish %.2f barrier %.2f gather %.2f "
            "heavy %.2f mix %.2f reduce %.2f\n",
            (int)blockIdx.x, G, r.nj, final_it, ph[0] * 0.01 / final_it, ph[1] * 0.01 / final_it,
            ph[2] * 0.01 / final_it, ph[3] * 0.01 / final_it, ph[4] * 0.01 / final_it, ph[5] * 0.01 / final_it,
@@ -588,7 +680,7 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
 }
 
 static int32_t hc_scratch(aiy_handle* h, int cals, int G, int cap) {
-  const size_t need = (size_t)cals * G * 2 * cap * sizeof(double) + (size_t)cals * G * 32 * 2 * sizeof(int) +
+  const size_t need = (size_t)cals * G * 2 * cap * sizeof(double) + (size_t)cals * G * 32 * 4 * sizeof(int) +
                       (size_t)cals * kHcCtrStride * sizeof(unsigned) + (size_t)cals * 2 * G * 4 * sizeof(double) +
                       256;
   if (need > h->hc_cap) {
@@ -623,7 +715,7 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   r.slab = reinterpret_cast<double*>(base);
   size_t off = (size_t)per_launch * p.G * 2 * p.cap * sizeof(double);
   r.span = reinterpret_cast<int*>(base + off);
-  off += (size_t)per_launch * p.G * 32 * 2 * sizeof(int);
+  off += (size_t)per_launch * p.G * 32 * 4 * sizeof(int);
   r.ctr = reinterpret_cast<unsigned*>(base + off);
   const size_t ctr_bytes = (size_t)per_launch * kHcCtrStride * sizeof(unsigned);
   off += ctr_bytes;
