@@ -57,13 +57,13 @@ class Market(ctypes.Structure):
 class PanelModel(ctypes.Structure):
     _fields_ = [("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32), ("n_lab", ctypes.c_int32),
                 ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp), ("mrkv_hist", vp),
-                ("act_T", ctypes.c_int32)]
+                ("act_T", ctypes.c_int32), ("unemployed", ctypes.c_int32)]
 
 
 class PanelBatch(ctypes.Structure):
     _fields_ = [("n_cal", ctypes.c_int32), ("S", ctypes.c_int32), ("n_M", ctypes.c_int32), ("n_a", ctypes.c_int32),
                 ("n_lab", ctypes.c_int32), ("tables", vp), ("M_grid", vp), ("lab_level", vp), ("lab_cdf", vp),
-                ("mrkv_hist", vp)]
+                ("mrkv_hist", vp), ("unemployed", ctypes.c_int32)]
 
 
 class StationaryModel(ctypes.Structure):
@@ -95,10 +95,11 @@ SIGNATURES = {
     "aiy_policy_eval": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp,
                                          ctypes.c_int64, vp, vp]),
     "aiy_sim_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market), ctypes.c_int64,
-                                         ctypes.c_int64, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_uint64,
-                                         ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]),
+                                         ctypes.c_int64, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, vp,
+                                         ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32,
+                                         ctypes.c_int32, vp, vp, vp, vp]),
     "aiy_sim_period_local": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.c_int64, ctypes.c_int64, vp, vp,
-                                              vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, vp, vp]),
+                                              vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, vp, vp]),
     "aiy_sim_period_prices": (ctypes.c_int32, [vp, ctypes.POINTER(PanelModel), ctypes.POINTER(Market),
                                                ctypes.c_int64, ctypes.c_int32, vp, vp, vp, vp]),
     "aiy_get_shocks": (ctypes.c_int32, [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp,
@@ -116,13 +117,13 @@ SIGNATURES = {
                                                 ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
     "aiy_sim_block_max_agents": (ctypes.c_int32, []),
     "aiy_sim_block_periods": (ctypes.c_int32, [vp, ctypes.POINTER(PanelBatch), vp, ctypes.c_int64, vp, vp, vp,
-                                               vp, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               vp, vp, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                vp, vp, vp, vp]),
     "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
     "aiy_index_ints_per_row": (ctypes.c_int32, []),
-    "aiy_panel_table_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "aiy_panel_table_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "aiy_panel_build": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                         ctypes.c_int32, vp, vp, vp, vp]),
+                                         ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp]),
     "aiy_build_index": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]),
     "aiy_comm_unique_id": (ctypes.c_int32, [vp]),
     "aiy_comm_init": (ctypes.c_int32, [vp, vp, ctypes.c_int32, ctypes.c_int32]),

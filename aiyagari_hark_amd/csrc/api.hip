@@ -4,7 +4,7 @@
 #include <cstring>
 #include <new>
 
-extern "C" int32_t aiy_version(void) { return 200; }  // 0.2.0
+extern "C" int32_t aiy_version(void) { return 210; }  // 0.2.1: Krusell-Smith employment
 
 extern "C" int32_t aiy_create(int32_t device, aiy_handle** out) {
   if (!out) return AIY_ERR_ARG;

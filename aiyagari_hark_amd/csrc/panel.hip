@@ -41,6 +41,8 @@ struct PanelRun {
   const double* u;   // uniforms [.. ][u_ld] starting at period u_t0, or nullptr (Philox)
   long long u_ld;
   int u_t0;
+  const uint8_t* emp;   // employment [..][emp_ld] from period u_t0, or nullptr (all employed)
+  long long emp_ld;
   unsigned long long seed;
   unsigned ge_iter;
   double* sow;
@@ -61,7 +63,7 @@ __device__ __forceinline__ void mill(const aiy_market& mk, const int* mrkv_hist,
   store_f64_agent(&sow[2], (double)p.Mrkv);
   store_f64_agent(&sow[3], p.Rnow);
   store_f64_agent(&sow[4], p.Wnow);
-  store_f64_agent(&sow[5], 0.0);  // Urate: everyone employed at UrateB = UrateG = 0
+  store_f64_agent(&sow[5], 0.0);  // Urate is recorded by the caller (it draws the employment)
   store_f64_agent(&sow[7], (double)(t + 1));
   if (hist_A) hist_A[t] = p.Aprev;
   if (hist_M) hist_M[t] = p.Mnow;
@@ -75,6 +77,7 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
   const int t = (int)load_f64_agent(&r.sow[7]);
   const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
   const double* u = r.u ? r.u + (size_t)(t - r.u_t0) * r.u_ld : nullptr;
+  const uint8_t* em = r.emp ? r.emp + (size_t)(t - r.u_t0) * r.emp_ld : nullptr;
   const int n_M = P.n_M, n_lab = P.n_lab, n_J = P.tab.g.n_J;
   // LinearInterpOnInterp1D bracket in M: the same for every agent of the period.
   int jc;
@@ -84,11 +87,12 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
   // LDS: the per-agent dependent chain then has no global hop before the policy lookup.
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
-  __shared__ CellHdr s_hdr[kLdsLab];
+  __shared__ CellHdr s_hdr[2 * kLdsLab];
   for (int q = threadIdx.x; q < n_lab * n_lab; q += blockDim.x) s_cdf[q] = P.lab_cdf[q];
   for (int q = threadIdx.x; q < n_lab; q += blockDim.x) {
     s_lvl[q] = P.lab_level[q];
-    s_hdr[q] = cell_header(P.tab, (2 * q + Mrkv) * n_J + jc);
+    s_hdr[q] = cell_header(P.tab, panel_cell(q, 1, Mrkv, n_lab, n_J, jc));
+    if (em) s_hdr[n_lab + q] = cell_header(P.tab, panel_cell(q, 0, Mrkv, n_lab, n_J, jc));
   }
   __syncthreads();
   double local = 0.0;
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
   for (long long pb = (long long)blockIdx.x * blockDim.x + threadIdx.x; pb < npairs; pb += nthreads * kPairs) {
     long long idx[kAgents];
     bool ok[kAgents];
-    int lp[kAgents], ln[kAgents];
+    int lp[kAgents], ln[kAgents], ev[kAgents];
     double ap[kAgents], m[kAgents], uu[kAgents];
 #pragma unroll
     for (int k = 0; k < kPairs; ++k) {
@@ -120,6 +124,8 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
         ap[2 * k] = ok[2 * k] ? r.a[i0] : 0.0; ap[2 * k + 1] = 0.0;
         lp[2 * k] = ok[2 * k] ? r.lab[i0] : 0; lp[2 * k + 1] = 0;
       }
+      ev[2 * k] = (em && ok[2 * k]) ? (int)em[i0] : 1;
+      ev[2 * k + 1] = (em && ok[2 * k + 1]) ? (int)em[i0 + 1] : 1;
       if (u) {
         uu[2 * k] = ok[2 * k] ? u[i0] : 0.0;
         uu[2 * k + 1] = ok[2 * k + 1] ? u[i0 + 1] : 0.0;
@@ -134,17 +140,18 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) uu[k] = 0.37 + 1e-9 * (double)(idx[k] & 1023);
 #endif
-    int cell[kAgents];
+    int cell[kAgents], hx[kAgents];
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
       int l = 0;
       for (int q = 0; q < n_lab; ++q) l += (s_cdf[lp[k] * n_lab + q] <= uu[k]) ? 1 : 0;  // searchsorted(cdf, u, 'right')
       ln[k] = l;
-      m[k] = Rnow * ap[k] + Wnow * (s_lvl[l] * 1.0);                                    // AS:1283
-      cell[k] = (2 * l + Mrkv) * n_J + jc;                                              // employed (Urate = 0)
+      m[k] = Rnow * ap[k] + Wnow * (s_lvl[l] * (double)ev[k]);                          // AS:1283
+      cell[k] = panel_cell(l, ev[k], Mrkv, n_lab, n_J, jc);                              // AS:1326-1356
+      hx[k] = panel_hdr(l, ev[k], n_lab);
     }
     double c[kAgents];
-    tab_policy<kAgents>(P.tab, cell, s_hdr, ln, m, alpha, n_M > 1, c);                          // AS:1326-1408
+    tab_policy<kAgents>(P.tab, cell, s_hdr, hx, m, alpha, n_M > 1, c);                          // AS:1326-1408
 #pragma unroll
     for (int k = 0; k < kAgents; ++k) {
       const double an = m[k] - c[k];                                                    // AS:1415
@@ -256,9 +263,9 @@ using namespace aiy;
 
 extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                                    int64_t n_local, int64_t agent_offset, int64_t n_total, double* a, uint8_t* lab,
-                                   const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter, int32_t t0,
-                                   int32_t n_periods, double* sow, double* hist_A, double* hist_M,
-                                   aiy_stream stream) {
+                                   const double* u, int64_t u_ld, const uint8_t* emp, int64_t emp_ld, uint64_t seed,
+                                   uint32_t ge_iter, int32_t t0, int32_t n_periods, double* sow, double* hist_A,
+                                   double* hist_M, aiy_stream stream) {
   if (!h) return AIY_ERR_ARG;
   if (!model || !mkt || !sow) return fail(h, AIY_ERR_ARG, "null model/market/sow");
   PanelDev P;
@@ -267,6 +274,8 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   if (n_local < 0 || n_total < 1 || agent_offset < 0) return fail(h, AIY_ERR_ARG, "bad agent counts");
   if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
   if (u && u_ld < n_local) return fail(h, AIY_ERR_ARG, "u_ld < n_local");
+  if (emp && emp_ld < n_local) return fail(h, AIY_ERR_ARG, "emp_ld < n_local");
+  if (emp && !P.unemployed) return fail(h, AIY_ERR_ARG, "employment states need tables with the unemployed cells");
   if (t0 < 0 || n_periods < 0 || t0 + (int64_t)n_periods > P.act_T)
     return fail(h, AIY_ERR_ARG, "bad period range [%d, %lld) for act_T=%d", t0, (long long)t0 + n_periods, P.act_T);
   if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
@@ -281,11 +290,14 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
   const int nb = sim_blocks(n_local);
   PanelRun r;
   r.n = n_local; r.offset = agent_offset; r.n_total = n_total; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld;
-  r.u_t0 = t0; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.u_t0 = t0; r.emp = emp; r.emp_ld = emp_ld; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow;
+  r.partials = h->d_partials; r.ticket = h->d_ticket;
   r.hist_A = hist_A; r.hist_M = hist_M; r.finish = h->comm ? 0 : 1;
   const aiy_market mk = *mkt;
 
-  if (!h->comm && h->use_resident && n_local >= kResMinAgents && resident_supported(P)) {
+  // the persistent kernel simulates the employed sub-states only (Krusell-Smith mode runs
+  // the per-period kernel)
+  if (!h->comm && h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P)) {
     // one persistent launch for the whole block of periods (panel_resident.hip)
     hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
     rc = launch_resident(h, P, mk, n_local, a, lab, u, u_ld, seed, ge_iter, t0, n_periods, sow, hist_A, hist_M, st);
@@ -328,8 +340,9 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
 
 // Two-step sharded period (caller-side all-reduce between the steps).
 extern "C" int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* model, int64_t n_local,
-                                        int64_t agent_offset, double* a, uint8_t* lab, const double* u, uint64_t seed,
-                                        uint32_t ge_iter, int32_t t, double* sow, aiy_stream stream) {
+                                        int64_t agent_offset, double* a, uint8_t* lab, const double* u,
+                                        const uint8_t* emp, uint64_t seed, uint32_t ge_iter, int32_t t, double* sow,
+                                        aiy_stream stream) {
   if (!h) return AIY_ERR_ARG;
   if (!sow) return fail(h, AIY_ERR_ARG, "null sow");
   PanelDev P;
@@ -339,6 +352,7 @@ extern "C" int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* mo
   if (n_local > 0 && (!a || !lab)) return fail(h, AIY_ERR_ARG, "null agent arrays");
   if (t < 0 || t >= P.act_T) return fail(h, AIY_ERR_ARG, "period t=%d outside [0, act_T=%d)", t, P.act_T);
   if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
+  if (emp && !P.unemployed) return fail(h, AIY_ERR_ARG, "employment states need tables with the unemployed cells");
   AIY_HIP(h, hipSetDevice(h->device));
   rc = ensure_panel_scratch(h);
   if (rc) return rc;
@@ -347,7 +361,7 @@ extern "C" int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* mo
   if (rc) return rc;
   PanelRun r;
   r.n = n_local; r.offset = agent_offset; r.n_total = n_local; r.a = a; r.lab = lab; r.u = u; r.u_ld = n_local;
-  r.u_t0 = t; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.u_t0 = t; r.emp = emp; r.emp_ld = n_local; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
   r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 0;
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t);
   if (n_local > 0) {
@@ -402,7 +416,7 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   if (rc) return rc;
   PanelRun r;
   r.n = n_local; r.offset = 0; r.n_total = n_local; r.a = a; r.lab = lab; r.u = nullptr; r.u_ld = 0; r.u_t0 = 0;
-  r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
+  r.emp = nullptr; r.emp_ld = 0; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
   r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 1;
   const int nb = sim_blocks(n_local);
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, 0);

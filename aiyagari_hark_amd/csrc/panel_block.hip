@@ -23,6 +23,7 @@ namespace aiy {
 
 struct BatchDev {
   int n_cal, S, n_M, n_a, n_lab, act_T;
+  bool unemployed;
   const char* tables;        // [n_cal][g.bytes] merged policy tables
   PanelTabGeom g;
   const double* M_grid;      // [n_cal][n_M]
@@ -36,6 +37,7 @@ struct BlockRun {
   double* a;                       // [n_cal][n]
   uint8_t* lab;                    // [n_cal][n]
   const double* u;                 // [n_cal][n_periods][n] or nullptr (Philox)
+  const uint8_t* emp;              // [n_cal][n_periods][n] or nullptr (all employed)
   const unsigned long long* seeds; // [n_cal]
   const aiy_market* mk;            // [n_cal]
   unsigned ge_iter;
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
 
   __shared__ double s_cdf[kLdsLab * kLdsLab];
   __shared__ double s_lvl[kLdsLab];
-  __shared__ CellHdr s_hdr[kLdsLab];
+  __shared__ CellHdr s_hdr[2 * kLdsLab];
   __shared__ double s_red[kBlkMaxThreads / kWave];
   __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
   for (int q = tid; q < n_lab * n_lab; q += nthr) s_cdf[q] = B.lab_cdf[(size_t)cal * n_lab * n_lab + q];
@@ -98,15 +100,19 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
     int jc;
     double alpha;
     m_bracket(Mg, n_M, Mnow, jc, alpha);
-    for (int q = tid; q < n_lab; q += nthr) s_hdr[q] = cell_header(T, (2 * q + Mrkv) * n_J + jc);
+    for (int q = tid; q < n_lab; q += nthr) {
+      s_hdr[q] = cell_header(T, panel_cell(q, 1, Mrkv, n_lab, n_J, jc));
+      if (r.emp) s_hdr[n_lab + q] = cell_header(T, panel_cell(q, 0, Mrkv, n_lab, n_J, jc));
+    }
     __syncthreads();
     const unsigned ctr0 = (r.ge_iter << 20) | (unsigned)t;
     const double* u = r.u ? r.u + ((size_t)cal * r.n_periods + p) * n : nullptr;
+    const uint8_t* em = r.emp ? r.emp + ((size_t)cal * r.n_periods + p) * n : nullptr;
     double local = 0.0;
     for (int g = tid; g < n_groups; g += nthr) {
       const int i0 = g * A;
       double m[A];
-      int ln[A];
+      int ln[A], ev[A];
 #pragma unroll
       for (int kk = 0; kk < A / 2; ++kk) {
         const int ia = i0 + 2 * kk;
@@ -125,16 +131,18 @@ __global__ __launch_bounds__(kBlkMaxThreads) void panel_block_kernel(BatchDev B,
           int l = 0;
           for (int q = 0; q < n_lab; ++q) l += (s_cdf[l0 * n_lab + q] <= uu[e]) ? 1 : 0;  // searchsorted 'right'
           ln[k] = l;
-          m[k] = Rnow * s_a[i] + Wnow * (s_lvl[l] * 1.0);                                // AS:1283
+          ev[k] = em ? (int)em[i] : 1;                                                    // EmpNow (AS:1222-1240)
+          m[k] = Rnow * s_a[i] + Wnow * (s_lvl[l] * (double)ev[k]);                      // AS:1283
         }
       }
-      int cell[A];
+      int cell[A], hx[A];
 #pragma unroll
       for (int k = 0; k < A; ++k) {
-        cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;                                        // employed (Urate = 0)
+        cell[k] = panel_cell(ln[k], ev[k], Mrkv, n_lab, n_J, jc);                      // AS:1326-1356
+        hx[k] = panel_hdr(ln[k], ev[k], n_lab);
       }
       double c[A];
-      tab_policy<A>(T, cell, s_hdr, ln, m, alpha, n_M > 1, c);                                  // AS:1326-1408
+      tab_policy<A>(T, cell, s_hdr, hx, m, alpha, n_M > 1, c);                                  // AS:1326-1408
 #pragma unroll
       for (int k = 0; k < A; ++k) {
         const int i = i0 + k;
@@ -188,7 +196,7 @@ extern "C" int32_t aiy_sim_block_max_agents(void) { return kBlkMaxAgents; }
 
 extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const aiy_market* markets,
                                          int64_t n_agents, double* a, uint8_t* lab, const double* u,
-                                         const uint64_t* seeds, uint32_t ge_iter, int32_t t0, int32_t n_periods,
+                                         const uint8_t* emp, const uint64_t* seeds, uint32_t ge_iter, int32_t t0, int32_t n_periods,
                                          int32_t act_T, double* sow, double* hist_A, double* hist_M,
                                          aiy_stream stream) {
   if (!h) return AIY_ERR_ARG;
@@ -201,6 +209,7 @@ extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* m
     return fail(h, AIY_ERR_ARG, "null batch model array (tables come from aiy_panel_build)");
   if (n_agents < 1 || n_agents > kBlkMaxAgents) return fail(h, AIY_ERR_UNSUPPORTED, "n_agents out of range");
   if (!a || !lab) return fail(h, AIY_ERR_ARG, "null agent arrays");
+  if (emp && !M.unemployed) return fail(h, AIY_ERR_ARG, "employment states need tables with the unemployed cells");
   if (t0 < 0 || n_periods < 0 || (int64_t)t0 + n_periods > act_T || act_T > (1 << 20))
     return fail(h, AIY_ERR_ARG, "bad period range");
   if (ge_iter >= (1u << 12)) return fail(h, AIY_ERR_ARG, "ge_iter too large for the Philox counter");
@@ -224,10 +233,12 @@ extern "C" int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* m
   AIY_HIP(h, hipMemcpyAsync(h->d_blk, h->h_blk, need, hipMemcpyHostToDevice, st));
   BatchDev B;
   B.n_cal = M.n_cal; B.S = M.S; B.n_M = M.n_M; B.n_a = M.n_a; B.n_lab = M.n_lab; B.act_T = act_T;
-  B.tables = static_cast<const char*>(M.tables); B.g = panel_tab_geom(M.n_lab, M.n_M, M.n_a); B.M_grid = M.M_grid;
+  B.unemployed = M.unemployed != 0;
+  B.tables = static_cast<const char*>(M.tables); B.g = panel_tab_geom(M.n_lab, M.n_M, M.n_a, B.unemployed);
+  B.M_grid = M.M_grid;
   B.lab_level = M.lab_level; B.lab_cdf = M.lab_cdf; B.mrkv_hist = M.mrkv_hist;
   BlockRun r;
-  r.n = n_agents; r.a = a; r.lab = lab; r.u = u;
+  r.n = n_agents; r.a = a; r.lab = lab; r.u = u; r.emp = emp;
   r.mk = reinterpret_cast<const aiy_market*>(h->d_blk);
   r.seeds = reinterpret_cast<const unsigned long long*>((char*)h->d_blk + sizeof(aiy_market) * M.n_cal);
   r.ge_iter = ge_iter; r.t0 = t0; r.n_periods = n_periods; r.sow = sow; r.hist_A = hist_A; r.hist_M = hist_M;

@@ -25,7 +25,9 @@ namespace aiy {
 //
 // Per-calibration layout (bytes; sections 256-aligned):
 //   rec [cells][Z + 1][4] double2 | z [cells][Z] double | idx [cells][buckets + 2] u64
-// cells = 2 n_lab n_J, n_J = max(n_M - 1, 1), cell(l, g, j) = (2 l + g) n_J + (j - 1).
+// cells = 2 n_lab n_J (employed sub-states only) or 4 n_lab n_J (with the unemployed
+// ones, Krusell-Smith mode), n_J = max(n_M - 1, 1); employed cell(l, g, j) =
+// (2 l + g) n_J + (j - 1), unemployed cell(l, g, j) = (2 n_lab + 2 l + g) n_J + (j - 1).
 // The index starts at z[2]: z[0] = z[1] is both rows' (1e-7, 1e-7) borrowing node
 // (AS:1503-1504), far below the first real node.
 // ---------------------------------------------------------------------------------
@@ -43,12 +45,12 @@ constexpr int kTabFirst = 2;   // first indexed node of z
 
 __host__ __device__ inline long long tab_align(long long b) { return (b + 255) / 256 * 256; }
 
-__host__ __device__ inline PanelTabGeom panel_tab_geom(int n_lab, int n_M, int n_a) {
+__host__ __device__ inline PanelTabGeom panel_tab_geom(int n_lab, int n_M, int n_a, bool unemployed = false) {
   PanelTabGeom g;
   g.n = n_a;
   g.Z = 2 * n_a;
   g.n_J = n_M > 1 ? n_M - 1 : 1;
-  g.n_cells = 2 * n_lab * g.n_J;
+  g.n_cells = (unemployed ? 4 : 2) * n_lab * g.n_J;
   int lg = 4;                                  // ~n_a buckets per octave (~Z / 2), 16 .. 8192
   while (lg < 13 && (1 << lg) < n_a) ++lg;
   g.shift = 52 - lg;
@@ -295,9 +297,18 @@ __device__ __forceinline__ void m_bracket(const double* __restrict__ Mg, int n_M
   }
 }
 
+// Cell of an agent with labour state l and employment e in aggregate state Mrkv, and the
+// index of its header among the period's staged headers (employed: l, unemployed:
+// n_lab + l).
+__device__ __forceinline__ int panel_cell(int l, int e, int Mrkv, int n_lab, int n_J, int jc) {
+  return (2 * l + Mrkv + (e ? 0 : 2 * n_lab)) * n_J + jc;
+}
+__device__ __forceinline__ int panel_hdr(int l, int e, int n_lab) { return e ? l : n_lab + l; }
+
 // One calibration's panel model on device (aiy_panel_model).
 struct PanelDev {
   int S, n_M, n_a, n_lab, act_T;
+  bool unemployed;   // tables hold the unemployed cells too
   const double* M_grid;
   const double* lab_level;
   const double* lab_cdf;

@@ -31,7 +31,10 @@ __global__ __launch_bounds__(256) void tab_merge_kernel(const double* __restrict
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e > 2 * n) return;
   const int lgc = cell / g.n_J, jc = cell - lgc * g.n_J;
-  const int s = 4 * (lgc >> 1) + 2 * (lgc & 1) + 1;   // employed sub-state of (l, g)
+  const int n_lg = 2 * (S / 4);                       // employed cells first, then the unemployed
+  const int emp = lgc < n_lg ? 1 : 0;
+  const int lg = emp ? lgc : lgc - n_lg;
+  const int s = 4 * (lg >> 1) + 2 * (lg & 1) + emp;   // sub-state 4 l + 2 g + emp (AS:1326-1356)
   const int j0 = n_M > 1 ? jc : 0, j1 = n_M > 1 ? jc + 1 : 0;
   const size_t r0 = (((size_t)cal * S + s) * n_M + j0) * n1;
   const size_t r1 = (((size_t)cal * S + s) * n_M + j1) * n1;
@@ -136,7 +139,8 @@ int32_t panel_dev(aiy_handle* h, const aiy_panel_model* model, PanelDev& P) {
   P.S = model->S; P.n_M = model->n_M; P.n_a = model->n_a; P.n_lab = model->n_lab; P.act_T = model->act_T;
   P.M_grid = model->M_grid; P.lab_level = model->lab_level; P.lab_cdf = model->lab_cdf;
   P.mrkv_hist = model->mrkv_hist;
-  P.tab = panel_tab(model->tables, panel_tab_geom(model->n_lab, model->n_M, model->n_a));
+  P.unemployed = model->unemployed != 0;
+  P.tab = panel_tab(model->tables, panel_tab_geom(model->n_lab, model->n_M, model->n_a, P.unemployed));
   return AIY_OK;
 }
 
@@ -144,13 +148,14 @@ int32_t panel_dev(aiy_handle* h, const aiy_panel_model* model, PanelDev& P) {
 
 using namespace aiy;
 
-extern "C" int64_t aiy_panel_table_bytes(int32_t n_lab, int32_t n_M, int32_t n_a) {
+extern "C" int64_t aiy_panel_table_bytes(int32_t n_lab, int32_t n_M, int32_t n_a, int32_t unemployed) {
   if (n_lab < 1 || n_lab > kLdsLab || n_M < 1 || n_a < 2 || 2LL * n_a >= BrkIdx::kMaxNodes) return -1;
-  return panel_tab_geom(n_lab, n_M, n_a).bytes;
+  return panel_tab_geom(n_lab, n_M, n_a, unemployed != 0).bytes;
 }
 
 extern "C" int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, int32_t n_a, int32_t n_lab,
-                                   const double* m_pol, const double* c_pol, void* tables, aiy_stream stream) {
+                                   int32_t unemployed, const double* m_pol, const double* c_pol, void* tables,
+                                   aiy_stream stream) {
   if (!h) return AIY_ERR_ARG;
   if (n_cal < 1 || n_cal > 65535 || n_M < 1 || n_a < 2 || n_lab < 1 || n_lab > kLdsLab || S != 4 * n_lab)
     return fail(h, AIY_ERR_ARG, "bad panel table sizes (n_cal=%d S=%d n_M=%d n_a=%d n_lab=%d)", n_cal, S, n_M, n_a,
@@ -159,7 +164,7 @@ extern "C" int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int3
   if (!m_pol || !c_pol || !tables) return fail(h, AIY_ERR_ARG, "null pointer");
   AIY_HIP(h, hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
-  const PanelTabGeom g = panel_tab_geom(n_lab, n_M, n_a);
+  const PanelTabGeom g = panel_tab_geom(n_lab, n_M, n_a, unemployed != 0);
   char* tabs = static_cast<char*>(tables);
   dim3 gm((2 * n_a + 1 + 255) / 256, g.n_cells, n_cal);
   hipLaunchKernelGGL(tab_merge_kernel, gm, dim3(256), 0, st, m_pol, c_pol, S, n_M, g, tabs);

@@ -151,8 +151,9 @@ class AiyagariType:
         self.solution_terminal = _Terminal(4 * self.LaborStatesNo, self.CRRA)
 
     def precompute_arrays(self):              # AS:906-1037
-        if self.UrateB != 0.0 or self.UrateG != 0.0:
-            raise NotImplementedError("UrateB/UrateG > 0 (full Krusell-Smith employment) is SURVEY §8f rank 2")
+        # Krusell-Smith mode (UrateB/UrateG > 0) needs nothing more here: the reference's
+        # household solve keeps LSStates as next-period labour income in the unemployed
+        # sub-states too (AS:990-1018), and L = (1 - Urate) LbrInd enters next_prices.
         self.egm_batch = EgmBatch.from_numpy(*self.egm_arrays(), device=self.device)
         self.add_to_time_inv("egm_batch")
 
@@ -218,11 +219,23 @@ class AiyagariType:
     def reset(self):                          # AS:1158
         self.initialize_sim()
 
+    @property
+    def ks_mode(self):
+        """Krusell-Smith employment (UrateB or UrateG > 0): exact-count employment
+        transitions each period (AS:1222-1240) and the unemployed sub-states' policies."""
+        return self.UrateB != 0.0 or self.UrateG != 0.0
+
     def initialize_sim(self):                 # AS:1164-1171 + [HARK] AgentType.initialize_sim
         self.shocks["Mrkv"] = self.MrkvInit
-        emp, lab = sm.birth_states(self.AgentCount, self.LaborStatesNo, self.UrateB, seed=self.seed)
+        emp, lab, self.RNG = sm.birth_states(self.AgentCount, self.LaborStatesNo, self.UrateB, seed=self.seed,
+                                             Mrkv=int(self.MrkvInit), UrateG=self.UrateG, with_rng=True)
         self.state_now["EmpNow"] = emp
         self.state_now["LaborSupplyState"] = lab
+        self._emp_host = emp
+        # make_emp_idx_arrays (AS:1171); the agent RNG above continues into the per-period
+        # employment permutations (the panel's employment is drawn on the host, exactly)
+        self.emp_trans = sm.employment_transitions(self.AgentCount, self.UrateB, self.UrateG, self.MrkvEmplArray,
+                                                   self.MrkvAggArray) if self.ks_mode else None
         self.t_sim = 0
         if self.panel is None or self.panel.n_local != self.AgentCount or self.panel.act_T != self.T_sim \
                 or self.panel.engine != self.panel_engine:
@@ -272,9 +285,21 @@ class AiyagariType:
                 cdf=torch.as_tensor(self.lab_cdf, dtype=torch.float64).to(dev),
                 n_lab=int(self.lab_cdf.shape[0]))
 
-    def get_shocks(self):                     # AS:1217-1256 (employment fixed: UrateB = UrateG = 0)
+    def employment_next(self, mrkv_now):
+        """This period's employment (get_shocks, AS:1222-1240) from the last one, host-side
+        with the agent RNG; everyone stays employed outside Krusell-Smith mode."""
+        if self.ks_mode:
+            self._emp_host = sm.employment_step(self._emp_host, mrkv_now, self.UrateB, self.emp_trans, self.RNG)
+        return self._emp_host
+
+    def get_shocks(self):                     # AS:1217-1256
         from . import _lib
         k = self._hook_const
+        if self.ks_mode:
+            emp = self.employment_next(self.shocks["Mrkv"])
+            self.state_now["EmpNow"] = torch.as_tensor(emp.astype(np.uint8)).to(self.device)
+        else:
+            self.state_now["EmpNow"] = self.state_prev["EmpNow"]
         lab = self.state_prev["LaborSupplyState"].clone()
         u = None
         if self.shock_mode == "numpy":   # np.random.choice per agent on the global RNG (AS:1254)
@@ -286,7 +311,6 @@ class AiyagariType:
                                                _lib.ptr(lab), _lib.ptr(u), int(self.shock_seed) & ((1 << 64) - 1),
                                                int(getattr(self, "ge_iter", 0)), int(self.t_sim), s), "aiy_get_shocks")
         self.state_now["LaborSupplyState"] = lab
-        self.state_now["EmpNow"] = self.state_prev["EmpNow"]
 
     def get_states(self):                     # AS:1259-1283
         from . import _lib
@@ -400,19 +424,36 @@ class AiyagariEconomy:
         lab_cdf = torch.as_tensor(agent.lab_cdf, dtype=torch.float64).to(agent.device)
         hist = torch.as_tensor(np.asarray(self.MrkvNow_hist, dtype=np.int32)).to(agent.device)
         market = self.market_constants()
-        p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, hist, market)
+        ks = agent.ks_mode
+        p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, hist, market, unemployed=ks)
         p.reset(agent.kInit, agent.state_now["LaborSupplyState"], self.sow_init["Mnow"], self.sow_init["Aprev"],
                 self.sow_init["Mrkv"], self.sow_init["Rnow"], self.sow_init["Wnow"])
         ge_iter = getattr(self, "_ge_iter", 0)
+        N = agent.AgentCount
+        urate = []
+        emp_src = None
+        if ks:
+            mrkv = np.asarray(self.MrkvNow_hist)
+            clock = [0]
+
+            def emp_src(n):   # EmpNow of the next n periods; the period's Mrkv is the sown one
+                out = np.empty((n, N), dtype=np.uint8)
+                for k in range(n):
+                    t = clock[0]
+                    now = self.sow_init["Mrkv"] if t == 0 else mrkv[t - 1]
+                    e = agent.employment_next(now)
+                    out[k] = e
+                    urate.append(1.0 - float(np.mean(e)))          # AS:1873 (recorded only)
+                    clock[0] = t + 1
+                return out
         if agent.shock_mode == "numpy":
-            N = agent.AgentCount
             src = lambda n: np.random.random_sample((n, N))  # noqa: E731 -- the reference's global RNG
-            p.run(0, self.act_T, shock_mode="numpy", u_host_source=src, ge_iter=ge_iter)
+            p.run(0, self.act_T, shock_mode="numpy", u_host_source=src, ge_iter=ge_iter, emp_source=emp_src)
         else:
-            p.run(0, self.act_T, shock_mode="philox", seed=agent.shock_seed, ge_iter=ge_iter)
+            p.run(0, self.act_T, shock_mode="philox", seed=agent.shock_seed, ge_iter=ge_iter, emp_source=emp_src)
         torch.cuda.synchronize(agent.device)
         self.store_history(agent, p.sow_host(), p.a.cpu().numpy(), p.lab.cpu().numpy(), p.hist_A.cpu().numpy(),
-                           p.hist_M.cpu().numpy())
+                           p.hist_M.cpu().numpy(), agent._emp_host if ks else None, urate if ks else None)
 
     # ---- [HARK] Market's per-period hooks ----------------------------------------------
     def make_history_hooks(self):
@@ -465,16 +506,19 @@ class AiyagariEconomy:
         return dict(CapShare=self.CapShare, DeprFac=self.DeprFac, prod=(self.ProdB, self.ProdG),
                     agg_L=((1.0 - self.UrateB) * self.LbrInd, (1.0 - self.UrateG) * self.LbrInd))
 
-    def store_history(self, agent, sow, aNow, lab, hist_A, hist_M):
+    def store_history(self, agent, sow, aNow, lab, hist_A, hist_M, emp=None, urate=None):
         """Write back one simulated history the way [HARK] Market.make_history leaves it."""
         self.Shk_idx = self.act_T
         for v in self.sow_vars:
             self.sow_state[v] = sow[v]
-        self.reap_state = {"aNow": [aNow], "EmpNow": [np.ones(agent.AgentCount)]}
+        emp = np.ones(agent.AgentCount) if emp is None else np.asarray(emp, dtype=np.float64)
+        self.reap_state = {"aNow": [aNow], "EmpNow": [emp]}
         agent.state_now["aNow"] = aNow
         agent.state_now["LaborSupplyState"] = lab.astype(np.int64)
+        agent.state_now["EmpNow"] = emp.astype(bool)
+        self.Urate = 1.0 - float(np.mean(emp))
         self.history = {"Mrkv": list(np.asarray(self.MrkvNow_hist[:self.act_T])), "Aprev": hist_A, "Mnow": hist_M,
-                        "Urate": np.zeros(self.act_T)}
+                        "Urate": np.zeros(self.act_T) if urate is None else np.asarray(urate)}
 
     def update_dynamics(self):                # [HARK] Market.update_dynamics
         dyn = self.calc_dynamics(Mnow=self.history["Mnow"], Aprev=self.history["Aprev"])

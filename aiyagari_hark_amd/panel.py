@@ -68,26 +68,32 @@ class DevicePanel:
         self.hist_A.zero_()
         self.hist_M.zero_()
 
-    def bind_model(self, m_pol, c_pol, M_grid, lab_level, lab_cdf, mrkv_hist, market: dict):
+    def bind_model(self, m_pol, c_pol, M_grid, lab_level, lab_cdf, mrkv_hist, market: dict, unemployed=False):
+        """unemployed: build the policy tables of the unemployed sub-states too (Krusell-Smith
+        mode: run(..., emp_source=...))."""
         S, n_M, n1 = m_pol.shape
         n_lab = int(lab_level.numel())
         keep = dict(M_grid=M_grid.contiguous(), lab_level=lab_level.contiguous(), lab_cdf=lab_cdf.contiguous(),
                     mrkv_hist=mrkv_hist.to(torch.int32).contiguous())
         # merged policy tables (aiy_panel_build, once per history)
         h = _lib.handle(self.device.index)
-        keep["tables"] = build_tables(h, m_pol[None], c_pol[None], n_lab, self.device)
+        keep["tables"] = build_tables(h, m_pol[None], c_pol[None], n_lab, self.device, unemployed)
         ptrs = [_lib.ptr(keep[k]) for k in ("tables", "M_grid", "lab_level", "lab_cdf", "mrkv_hist")]
         # periods a call may simulate: the history buffers and the Mrkv history must cover them
         self.model_T = min(self.act_T, int(keep["mrkv_hist"].numel()))
-        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *ptrs, self.model_T)
+        pm = _lib.PanelModel(S, n_M, n1 - 1, n_lab, *ptrs, self.model_T, int(bool(unemployed)))
         mk = make_market(market)
-        pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *ptrs)
+        pb = _lib.PanelBatch(1, S, n_M, n1 - 1, n_lab, *ptrs, int(bool(unemployed)))
         self._model = (pm, mk, keep, pb)
 
     def run(self, t0: int, n_periods: int, shock_mode="philox", seed=0, ge_iter=0, u_host_source=None,
-            chunk=1000, stream=None, allreduce=None):
+            chunk=1000, stream=None, allreduce=None, emp_source=None):
         """Simulate periods [t0, t0 + n_periods).  For shock_mode='numpy', u_host_source(n)
         must return the next n x n_local uniforms (host).
+
+        emp_source: Krusell-Smith mode (bind_model(unemployed=True)): emp_source(n) returns
+        the employment states (0/1) of the next n periods, [n, n_local] (host); None:
+        everyone employed.
 
         allreduce: for an agent-sharded panel without a communicator bound in the library
         (parallel.bind_rccl), a callable that sums the 1-element device tensor it is given
@@ -98,74 +104,73 @@ class DevicePanel:
             raise RuntimeError("bind_model() first")
         if t0 < 0 or n_periods < 0 or t0 + n_periods > self.model_T:
             raise ValueError(f"periods [{t0}, {t0 + n_periods}) outside the history [0, {self.model_T})")
+        if shock_mode not in ("philox", "numpy"):
+            raise ValueError(shock_mode)
         pm, mk, _, pb = self._model
+        if emp_source is not None and not pm.unemployed:
+            raise ValueError("employment states need bind_model(..., unemployed=True)")
         h = _lib.handle(self.device.index)
         sp = _lib.stream_ptr(stream)
         if allreduce is not None:
             self._run_stepwise(h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
-                               allreduce)
+                               allreduce, emp_source)
             return
         if self._engine(h) == "block":
             if self.n_total != self.n_local or self.agent_offset != 0:
                 raise ValueError("the block engine does not shard agents")
             seeds = (ctypes.c_uint64 * 1)(int(seed) & ((1 << 64) - 1))
             run_block(h, pb, ctypes.byref(mk), self.n_local, self.a, self.lab, seeds, ge_iter, t0, n_periods,
-                      self.act_T, self.sow, self.hist_A, self.hist_M, shock_mode, u_host_source, chunk, sp, stream)
+                      self.act_T, self.sow, self.hist_A, self.hist_M, shock_mode, u_host_source, chunk, sp, stream,
+                      emp_source)
             return
-        if shock_mode == "philox":
+        if shock_mode == "philox" and emp_source is None:
             h.check(h.lib.aiy_sim_periods(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_local, self.agent_offset,
-                                          self.n_total, _lib.ptr(self.a), _lib.ptr(self.lab), None, 0,
+                                          self.n_total, _lib.ptr(self.a), _lib.ptr(self.lab), None, 0, None, 0,
                                           int(seed) & ((1 << 64) - 1), int(ge_iter), int(t0), int(n_periods),
                                           _lib.ptr(self.sow), _lib.ptr(self.hist_A), _lib.ptr(self.hist_M), sp),
                     "aiy_sim_periods")
             return
-        if shock_mode != "numpy":
-            raise ValueError(shock_mode)
         t = t0
         end = t0 + n_periods
         while t < end:
             n = min(chunk, end - t)
-            u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
-            if u.shape != (n, self.n_local):
-                raise ValueError(f"u block shape {u.shape} != {(n, self.n_local)}")
-            ud = torch.from_numpy(u).to(self.device, non_blocking=False)
+            ud = _host_block(u_host_source, n, (n, self.n_local), np.float64, self.device) \
+                if shock_mode == "numpy" else None
+            ed = _host_block(emp_source, n, (n, self.n_local), np.uint8, self.device) if emp_source else None
             h.check(h.lib.aiy_sim_periods(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_local, self.agent_offset,
                                           self.n_total, _lib.ptr(self.a), _lib.ptr(self.lab), _lib.ptr(ud),
-                                          self.n_local, 0, int(ge_iter), int(t), int(n), _lib.ptr(self.sow),
+                                          self.n_local, _lib.ptr(ed), self.n_local, int(seed) & ((1 << 64) - 1),
+                                          int(ge_iter), int(t), int(n), _lib.ptr(self.sow),
                                           _lib.ptr(self.hist_A), _lib.ptr(self.hist_M), sp), "aiy_sim_periods")
             torch.cuda.current_stream(self.device).synchronize() if stream is None else stream.synchronize()
-            del ud
+            del ud, ed
             t += n
 
     def _run_stepwise(self, h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
-                      allreduce):
+                      allreduce, emp_source=None):
         """Sharded periods with the all-reduce done by the caller between the library's two
         steps (Aiyagari_Support.py:1868, np.mean over all ranks' agents)."""
-        if shock_mode not in ("philox", "numpy"):
-            raise ValueError(shock_mode)
         red = self.sow[6:7]
         t, end = t0, t0 + n_periods
         while t < end:
             n = min(chunk, end - t)
-            ud = None
-            if shock_mode == "numpy":
-                u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
-                if u.shape != (n, self.n_local):
-                    raise ValueError(f"u block shape {u.shape} != {(n, self.n_local)}")
-                ud = torch.from_numpy(u).to(self.device)
+            ud = _host_block(u_host_source, n, (n, self.n_local), np.float64, self.device) \
+                if shock_mode == "numpy" else None
+            ed = _host_block(emp_source, n, (n, self.n_local), np.uint8, self.device) if emp_source else None
             for k in range(n):
                 up = None if ud is None else ud[k].data_ptr()
+                ep = None if ed is None else ed[k].data_ptr()
                 h.check(h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), self.n_local, self.agent_offset,
-                                                   _lib.ptr(self.a), _lib.ptr(self.lab), up,
+                                                   _lib.ptr(self.a), _lib.ptr(self.lab), up, ep,
                                                    int(seed) & ((1 << 64) - 1), int(ge_iter), int(t + k),
                                                    _lib.ptr(self.sow), sp), "aiy_sim_period_local")
                 allreduce(red)
                 h.check(h.lib.aiy_sim_period_prices(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_total, int(t + k),
                                                     _lib.ptr(self.sow), _lib.ptr(self.hist_A), _lib.ptr(self.hist_M),
                                                     sp), "aiy_sim_period_prices")
-            if ud is not None:
+            if ud is not None or ed is not None:
                 torch.cuda.current_stream(self.device).synchronize()
-                del ud
+            del ud, ed
             t += n
 
     def sow_host(self):
@@ -174,53 +179,68 @@ class DevicePanel:
                     Urate=float(s[5]))
 
 
+def _host_block(source, n, shape, dtype, device):
+    """The next n periods of a host-side source (uniforms / employment) as a device tensor
+    of `shape` (one calibration) or [n_cal, *shape] (batched)."""
+    x = np.ascontiguousarray(source(n), dtype=dtype)
+    if x.shape != shape:
+        raise ValueError(f"host block shape {x.shape} != {shape}")
+    return torch.from_numpy(x).to(device)
+
+
 def make_market(market: dict) -> "_lib.Market":
     return _lib.Market(market["CapShare"], market["DeprFac"], (ctypes.c_double * 2)(*market["prod"]),
                        (ctypes.c_double * 2)(*market["agg_L"]))
 
 
-def build_tables(h, m_pol, c_pol, n_lab, device):
+def build_tables(h, m_pol, c_pol, n_lab, device, unemployed=False):
     """Merged policy tables of n_cal calibrations (aiy_panel_build): m_pol/c_pol
-    [n_cal, S, n_M, n_a + 1] device tensors -> uint8 tensor [n_cal, table bytes]."""
+    [n_cal, S, n_M, n_a + 1] device tensors -> uint8 tensor [n_cal, table bytes]
+    (unemployed: with the unemployed sub-states' cells, Krusell-Smith mode)."""
     n_cal, S, n_M, n1 = m_pol.shape
-    nbytes = int(h.lib.aiy_panel_table_bytes(n_lab, n_M, n1 - 1))
+    nbytes = int(h.lib.aiy_panel_table_bytes(n_lab, n_M, n1 - 1, int(bool(unemployed))))
     if nbytes <= 0:
         raise _lib.AiyagariLibError(f"unsupported panel table sizes n_lab={n_lab} n_M={n_M} n_a={n1 - 1}")
     tables = torch.empty((n_cal, nbytes), dtype=torch.uint8, device=device)
     m_pol = m_pol.contiguous()
     c_pol = c_pol.contiguous()
-    h.check(h.lib.aiy_panel_build(h.h, n_cal, S, n_M, n1 - 1, n_lab, _lib.ptr(m_pol), _lib.ptr(c_pol),
-                                  _lib.ptr(tables), _lib.stream_ptr()), "aiy_panel_build")
+    h.check(h.lib.aiy_panel_build(h.h, n_cal, S, n_M, n1 - 1, n_lab, int(bool(unemployed)), _lib.ptr(m_pol),
+                                  _lib.ptr(c_pol), _lib.ptr(tables), _lib.stream_ptr()), "aiy_panel_build")
     return tables
 
 
 def run_block(h, pb, markets_ref, n_agents, a, lab, seeds, ge_iter, t0, n_periods, act_T, sow, hist_A, hist_M,
-              shock_mode, u_host_source, chunk, sp, stream):
+              shock_mode, u_host_source, chunk, sp, stream, emp_source=None):
     """aiy_sim_block_periods over [t0, t0 + n_periods): Philox in one call, host uniforms
-    in chunks of ``chunk`` periods (u_host_source(n) -> [n_cal][n][n_agents] or, for one
-    calibration, [n][n_agents])."""
-    if shock_mode == "philox":
+    (u_host_source(n) -> [n_cal][n][n_agents] or, for one calibration, [n][n_agents]) and
+    employment states (emp_source, same shapes) in chunks of ``chunk`` periods."""
+    if shock_mode == "philox" and emp_source is None:
         h.check(h.lib.aiy_sim_block_periods(h.h, ctypes.byref(pb), markets_ref, n_agents, _lib.ptr(a), _lib.ptr(lab),
-                                            None, seeds, int(ge_iter), int(t0), int(n_periods), int(act_T),
+                                            None, None, seeds, int(ge_iter), int(t0), int(n_periods), int(act_T),
                                             _lib.ptr(sow), _lib.ptr(hist_A), _lib.ptr(hist_M), sp),
                 "aiy_sim_block_periods")
         return
-    if shock_mode != "numpy":
+    if shock_mode not in ("philox", "numpy"):
         raise ValueError(shock_mode)
+
+    def block(source, n, dtype):
+        x = np.ascontiguousarray(source(n), dtype=dtype)
+        want = (pb.n_cal, n, n_agents)
+        if x.shape != want and not (pb.n_cal == 1 and x.shape == want[1:]):
+            raise ValueError(f"host block shape {x.shape} != {want}")
+        return torch.from_numpy(x.reshape(want)).to(a.device)
+
     t, end = t0, t0 + n_periods
     while t < end:
         n = min(chunk, end - t)
-        u = np.ascontiguousarray(u_host_source(n), dtype=np.float64)
-        want = (pb.n_cal, n, n_agents)
-        if u.shape != want and not (pb.n_cal == 1 and u.shape == want[1:]):
-            raise ValueError(f"u block shape {u.shape} != {want}")
-        ud = torch.from_numpy(u.reshape(want)).to(a.device)
+        ud = block(u_host_source, n, np.float64) if shock_mode == "numpy" else None
+        ed = block(emp_source, n, np.uint8) if emp_source is not None else None
         h.check(h.lib.aiy_sim_block_periods(h.h, ctypes.byref(pb), markets_ref, n_agents, _lib.ptr(a), _lib.ptr(lab),
-                                            _lib.ptr(ud), seeds, int(ge_iter), int(t), int(n), int(act_T),
-                                            _lib.ptr(sow), _lib.ptr(hist_A), _lib.ptr(hist_M), sp),
+                                            _lib.ptr(ud), _lib.ptr(ed), seeds, int(ge_iter), int(t), int(n),
+                                            int(act_T), _lib.ptr(sow), _lib.ptr(hist_A), _lib.ptr(hist_M), sp),
                 "aiy_sim_block_periods")
         torch.cuda.current_stream(a.device).synchronize() if stream is None else stream.synchronize()
-        del ud
+        del ud, ed
         t += n
 
 
@@ -266,7 +286,7 @@ class BatchedPanel:
         keep["tables"] = build_tables(h, m_pol, c_pol, n_lab, self.device)
         pb = _lib.PanelBatch(n_cal, S, n_M, n1 - 1, n_lab, *(_lib.ptr(keep[k]) for k in
                                                               ("tables", "M_grid", "lab_level", "lab_cdf",
-                                                               "mrkv_hist")))
+                                                               "mrkv_hist")), 0)
         mks = (_lib.Market * n_cal)(*(make_market(m) for m in markets))
         self._model = (pb, mks, keep)
 

@@ -162,15 +162,59 @@ def choice_cdf_table(P):
     return out
 
 
-def birth_states(AgentCount, n_lab, UrateB, seed=0):
+def birth_states(AgentCount, n_lab, UrateB, seed=0, Mrkv=0, UrateG=None, with_rng=False):
     """sim_birth (AS:1173-1214) after [HARK] reset_rng: RandomState(seed); employment
-    permutation, then the even labour split permuted (two RNG.permutation calls)."""
+    permutation (unemployment count of the birth period's macro state), then the even
+    labour split permuted (two RNG.permutation calls).  with_rng: also return the agent
+    RNG, which the per-period employment permutations continue (AS:1239-1240)."""
     if AgentCount % n_lab != 0:
         raise ValueError("AgentCount must be a multiple of LaborStatesNo (AS:757, AS:1203)")
+    if Mrkv not in (0, 1):
+        raise ValueError("Illegal macroeconomic state: MrkvNow must be 0 or 1")   # AS:1191-1192
+    rate = UrateB if Mrkv == 0 or UrateG is None else UrateG
     rng = np.random.RandomState(seed)
-    unemp = int(np.round(UrateB * AgentCount))
+    unemp = int(np.round(rate * AgentCount))
     emp = np.concatenate([np.zeros(unemp, dtype=bool), np.ones(AgentCount - unemp, dtype=bool)])
     lab = np.repeat(np.arange(n_lab), AgentCount // n_lab)
     emp = rng.permutation(emp)
     lab = rng.permutation(lab)
-    return emp, lab
+    return (emp, lab, rng) if with_rng else (emp, lab)
+
+
+def employment_transitions(AgentCount, UrateB, UrateG, MrkvEmplArray, MrkvAggArray):
+    """make_emp_idx_arrays (AS:1042-1156): for each macro transition j -> k the 0/1 arrays
+    whose permutations assign this period's employment to last period's employed
+    ("emp") and unemployed ("unemp") agents, so each state's unemployment count is exact.
+    stay counts = round(previous count x P(stay | j -> k)) with the reference's operand
+    order; the movers make up the new state's count."""
+    unemp = [int(np.round(UrateB * AgentCount)), int(np.round(UrateG * AgentCount))]
+    emp = [AgentCount - unemp[0], AgentCount - unemp[1]]
+    out = {"emp": [[None, None], [None, None]], "unemp": [[None, None], [None, None]]}
+    for j in (0, 1):
+        for k in (0, 1):
+            stay_u = int(np.round(unemp[j] * MrkvEmplArray[2 * j, 2 * k] / MrkvAggArray[j, k]))
+            stay_e = int(np.round(emp[j] * (MrkvEmplArray[2 * j + 1, 2 * k + 1]) / MrkvAggArray[j, k]))
+            to_u, to_e = unemp[k] - stay_u, emp[k] - stay_e
+            out["emp"][j][k] = np.r_[np.ones(stay_e, dtype=bool), np.zeros(to_u, dtype=bool)]
+            out["unemp"][j][k] = np.r_[np.ones(to_e, dtype=bool), np.zeros(stay_u, dtype=bool)]
+    return out
+
+
+def employment_step(emp_prev, mrkv_now, UrateB, trans, rng):
+    """get_shocks' employment update (AS:1222-1240): previous macro state from last
+    period's unemployment rate (compared with UrateB as a float, AS:1227), then one
+    permutation for the employed and one for the unemployed (agent RNG, in that order).
+    A transition array whose length differs from its group raises, as the reference's
+    boolean assignment does."""
+    was = np.asarray(emp_prev, dtype=bool)
+    mrkv_prev = int(((~was).sum() / float(was.size)) != UrateB)
+    e_arr, u_arr = trans["emp"][mrkv_prev][int(mrkv_now)], trans["unemp"][mrkv_prev][int(mrkv_now)]
+    n_e = int(was.sum())
+    if e_arr.size != n_e or u_arr.size != was.size - n_e:
+        raise ValueError(f"employment transition {mrkv_prev}->{int(mrkv_now)}: arrays of {e_arr.size}/{u_arr.size} "
+                         f"for {n_e} employed / {was.size - n_e} unemployed agents (AgentCount does not give exact "
+                         "counts for these unemployment rates)")
+    now = np.empty(was.size, dtype=bool)
+    now[was] = rng.permutation(e_arr)
+    now[~was] = rng.permutation(u_arr)
+    return now

@@ -156,11 +156,14 @@ typedef struct {
   const int32_t* mrkv_hist; /* [act_T] MrkvNow_hist (AS:1793-1805)                          */
   int32_t act_T;            /* length of mrkv_hist and of the hist_A / hist_M buffers: every
                                call is checked to simulate periods t0 + n_periods <= act_T   */
+  int32_t unemployed;       /* != 0: tables built with the unemployed sub-states too
+                               (Krusell-Smith mode, UrateB/UrateG > 0)                       */
 } aiy_panel_model;
 
 /* Panel policy tables (get_controls, AS:1326-1408).  Each period an agent of labour
- * state l evaluates LinearInterpOnInterp1D = (1 - alpha) f_{j-1}(m) + alpha f_j(m) of
- * its employed sub-state s = 4 l + 2 Mrkv + 1.  For every (l, Mrkv, M interval j) the
+ * state l and employment e evaluates LinearInterpOnInterp1D = (1 - alpha) f_{j-1}(m) +
+ * alpha f_j(m) of its sub-state s = 4 l + 2 Mrkv + e (e = 1 only unless `unemployed`).
+ * For every (l, Mrkv, e, M interval j) the
  * two rows' nodes are merged into one sorted list; on each merged segment both rows'
  * brackets are fixed, so one 64-byte record holds both, and a bracket index over the
  * merged nodes (log buckets, one 64-bit entry each) finds the record with no search
@@ -169,9 +172,10 @@ typedef struct {
  *   aiy_panel_table_bytes: bytes of ONE calibration's tables (-1: unsupported sizes)
  *   aiy_panel_build: m_pol, c_pol [n_cal][S][n_M][n_a+1] (device) -> tables
  *                    [n_cal][aiy_panel_table_bytes] (device).  Asynchronous. */
-int64_t aiy_panel_table_bytes(int32_t n_lab, int32_t n_M, int32_t n_a);
+int64_t aiy_panel_table_bytes(int32_t n_lab, int32_t n_M, int32_t n_a, int32_t unemployed);
 int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, int32_t n_a, int32_t n_lab,
-                        const double* m_pol, const double* c_pol, void* tables, aiy_stream stream);
+                        int32_t unemployed, const double* m_pol, const double* c_pol, void* tables,
+                        aiy_stream stream);
 
 /* Device-resident market state ("sow_state", AS:1585), 8 doubles:
  *   [0] Mnow [1] Aprev [2] Mrkv [3] Rnow [4] Wnow [5] Urate [6] sum(a) [7] period index t */
@@ -188,6 +192,10 @@ int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, in
  *   u: NULL -> on-device Philox4x32-10 (counter (ge_iter<<20 | t, idx, 0), key seed),
  *      else host-supplied uniforms [n_periods][u_ld] starting at period t0 (parity
  *      with np.random.choice)
+ *   emp: NULL -> everyone employed (UrateB = UrateG = 0), else the employment states
+ *      (uint8 0/1, device) [n_periods][emp_ld] from period t0 -- this period's EmpNow of
+ *      get_shocks (AS:1222-1240; exact-count permutations drawn with the agent RNG by the
+ *      caller).  Needs tables with the unemployed cells (model->unemployed).
  *   agent_offset: global index of local agent 0 (Philox counter, sharding)
  * With a communicator bound (aiy_comm_init) the per-period sum of a is all-reduced
  * over RCCL before the prices are formed; otherwise n_local must equal n_total (or use
@@ -196,9 +204,9 @@ int32_t aiy_panel_build(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_M, in
  * (single rank, n_periods >= 128) return after the periods completed. */
 int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                         int64_t n_local, int64_t agent_offset, int64_t n_total, double* a,
-                        uint8_t* lab, const double* u, int64_t u_ld, uint64_t seed, uint32_t ge_iter,
-                        int32_t t0, int32_t n_periods, double* sow, double* hist_A, double* hist_M,
-                        aiy_stream stream);
+                        uint8_t* lab, const double* u, int64_t u_ld, const uint8_t* emp, int64_t emp_ld,
+                        uint64_t seed, uint32_t ge_iter, int32_t t0, int32_t n_periods, double* sow,
+                        double* hist_A, double* hist_M, aiy_stream stream);
 
 /* One sharded period in two steps with the all-reduce left to the caller (any backend:
  * torch.distributed over RCCL or gloo, MPI, ...): the agent-sharded form of
@@ -206,14 +214,15 @@ int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_m
  *   aiy_sim_period_local:  period t of the n_local agents (get_shocks .. get_poststates,
  *                          AS:1217-1415); leaves their sum of a in sow[6] (device).
  *                          u: NULL (Philox by global index) or n_local host uniforms of
- *                          period t.
+ *                          period t; emp: NULL or the n_local employment states of t.
  *   -- caller: sow[6] <- sum over ranks of sow[6] --
  *   aiy_sim_period_prices: mill / calc_R_and_W (AS:1839-1894) on sow[6] / n_total; writes
  *                          sow, hist_A[t], hist_M[t] and advances sow[7] to t + 1.
  * Both asynchronous on `stream`. */
 int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* model, int64_t n_local,
                              int64_t agent_offset, double* a, uint8_t* lab, const double* u,
-                             uint64_t seed, uint32_t ge_iter, int32_t t, double* sow, aiy_stream stream);
+                             const uint8_t* emp, uint64_t seed, uint32_t ge_iter, int32_t t, double* sow,
+                             aiy_stream stream);
 int32_t aiy_sim_period_prices(aiy_handle* h, const aiy_panel_model* model, const aiy_market* mkt,
                               int64_t n_total, int32_t t, double* sow, double* hist_A, double* hist_M,
                               aiy_stream stream);
@@ -279,6 +288,7 @@ typedef struct {
   const double* lab_level;  /* [n_cal][n_lab] */
   const double* lab_cdf;    /* [n_cal][n_lab][n_lab] */
   const int32_t* mrkv_hist; /* [n_cal][act_T] */
+  int32_t unemployed;       /* != 0: tables with the unemployed sub-states (aiy_panel_build) */
 } aiy_panel_batch;
 
 /* Largest per-calibration population aiy_sim_block_periods accepts. */
@@ -289,12 +299,14 @@ int32_t aiy_sim_block_max_agents(void);
  *   a [n_cal][n_agents], lab [n_cal][n_agents] uint8 (device, in/out)
  *   u: NULL -> Philox (counter (ge_iter<<20 | t, idx/2, 0), key seeds[c]), else host
  *      uniforms [n_cal][n_periods][n_agents]
+ *   emp: NULL (everyone employed) or employment states [n_cal][n_periods][n_agents]
+ *      (uint8, device; as aiy_sim_periods)
  *   sow [n_cal][AIY_SOW_DOUBLES] (device, in/out); hist_A/hist_M [n_cal][act_T] or NULL.
  * Asynchronous (the call waits for earlier work on `stream` before it refills its
  * pinned staging buffer). */
 int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const aiy_market* markets,
                               int64_t n_agents, double* a, uint8_t* lab, const double* u,
-                              const uint64_t* seeds, uint32_t ge_iter, int32_t t0, int32_t n_periods,
+                              const uint8_t* emp, const uint64_t* seeds, uint32_t ge_iter, int32_t t0, int32_t n_periods,
                               int32_t act_T, double* sow, double* hist_A, double* hist_M,
                               aiy_stream stream);
 

@@ -513,14 +513,21 @@ def egm_solve(DiscFac, CRRA, aGrid, Mgrid, Rk, Wk, Mk, LSStates, P, tol=AGENT_TO
 # --------------------------------------------------------------------------------------
 # Panel simulation (rows B1-B6)
 # --------------------------------------------------------------------------------------
-def sim_birth_labor(AgentCount, LaborStatesNo, UrateB, seed=0, Mrkv=0):
+def sim_birth_labor(AgentCount, LaborStatesNo, UrateB, seed=0, Mrkv=0, UrateG=None, return_rng=False):
     """initialize_sim / sim_birth (AS:1164-1214) with [HARK] reset_rng (RandomState(seed)).
 
-    Returns (EmpNow bool[N], LaborSupplyState int[N]).  Two RNG.permutation calls, in the
-    reference's order (AS:1212, AS:1214)."""
+    Returns (EmpNow bool[N], LaborSupplyState int[N]) -- and the agent RNG, which the
+    per-period employment permutations continue (AS:1239-1240), if return_rng.  Two
+    RNG.permutation calls, in the reference's order (AS:1212, AS:1214); the unemployment
+    count is the birth period's state's (AS:1185-1190)."""
     rng = np.random.RandomState(seed)
     N = AgentCount
-    unemp_N = int(np.round(UrateB * N))
+    if Mrkv == 0:
+        unemp_N = int(np.round(UrateB * N))
+    elif Mrkv == 1:
+        unemp_N = int(np.round((UrateB if UrateG is None else UrateG) * N))
+    else:
+        raise ValueError("Illegal macroeconomic state: MrkvNow must be 0 or 1")
     emp_N = AgentCount - unemp_N
     EmpNew = np.concatenate([np.zeros(unemp_N, dtype=bool), np.ones(emp_N, dtype=bool)])
     LSNew = np.empty(0)
@@ -529,7 +536,57 @@ def sim_birth_labor(AgentCount, LaborStatesNo, UrateB, seed=0, Mrkv=0):
     LSNew2 = np.array([int(el) for el in LSNew])
     emp = rng.permutation(EmpNew)
     lab = rng.permutation(LSNew2)
+    if return_rng:
+        return emp, lab, rng
     return emp, lab
+
+
+def make_emp_idx_arrays(AgentCount, UrateB, UrateG, MrkvEmplArray, MrkvAggArray):
+    """AiyagariType.make_emp_idx_arrays (AS:1042-1156): emp_permute[j][k] / unemp_permute[j][k]
+    are the boolean arrays whose random permutations give, for the macro transition j -> k,
+    this period's employment of last period's employed / unemployed agents (exact counts).
+    Written out per transition as the reference does (same products, same rounding)."""
+    E, A = MrkvEmplArray, MrkvAggArray
+    B_unemp_N = int(np.round(UrateB * AgentCount))
+    B_emp_N = AgentCount - B_unemp_N
+    G_unemp_N = int(np.round(UrateG * AgentCount))
+    G_emp_N = AgentCount - G_unemp_N
+
+    def pair(stay_emp, become_unemp, become_emp, stay_unemp):
+        unemp_p = np.concatenate([np.ones(become_emp, dtype=bool), np.zeros(stay_unemp, dtype=bool)])
+        emp_p = np.concatenate([np.ones(stay_emp, dtype=bool), np.zeros(become_unemp, dtype=bool)])
+        return emp_p, unemp_p
+
+    BB_stay_unemp_N = int(np.round(B_unemp_N * E[0, 0] / A[0, 0]))
+    BB_stay_emp_N = int(np.round(B_emp_N * (E[1, 1]) / A[0, 0]))
+    BB = pair(BB_stay_emp_N, B_unemp_N - BB_stay_unemp_N, B_emp_N - BB_stay_emp_N, BB_stay_unemp_N)
+    BG_stay_unemp_N = int(np.round(B_unemp_N * E[0, 2] / A[0, 1]))
+    BG_stay_emp_N = int(np.round(B_emp_N * (E[1, 3]) / A[0, 1]))
+    BG = pair(BG_stay_emp_N, G_unemp_N - BG_stay_unemp_N, G_emp_N - BG_stay_emp_N, BG_stay_unemp_N)
+    GB_stay_unemp_N = int(np.round(G_unemp_N * E[2, 0] / A[1, 0]))
+    GB_stay_emp_N = int(np.round(G_emp_N * E[3, 1] / A[1, 0]))
+    GB = pair(GB_stay_emp_N, B_unemp_N - GB_stay_unemp_N, B_emp_N - GB_stay_emp_N, GB_stay_unemp_N)
+    GG_stay_unemp_N = int(np.round(G_unemp_N * E[2, 2] / A[1, 1]))
+    GG_stay_emp_N = int(np.round(G_emp_N * E[3, 3] / A[1, 1]))
+    GG = pair(GG_stay_emp_N, G_unemp_N - GG_stay_unemp_N, G_emp_N - GG_stay_emp_N, GG_stay_unemp_N)
+    return dict(emp=[[BB[0], BG[0]], [GB[0], GG[0]]], unemp=[[BB[1], BG[1]], [GB[1], GG[1]]])
+
+
+def employment_step(emp_prev, mrkv_now, UrateB, perms, rng):
+    """get_shocks employment part (AS:1222-1240): the previous macro state is read off
+    last period's unemployment rate (AS:1227, a float comparison with UrateB), then the
+    employed and the unemployed are each given a permutation of their transition array
+    (agent RNG, employed first).  Raises like NumPy's boolean assignment does when an
+    array's length differs from the group it is assigned to."""
+    employed = np.asarray(emp_prev).astype(bool)
+    unemployed = np.logical_not(employed)
+    mrkv_prev = int((unemployed.sum() / float(employed.size)) != UrateB)
+    emp_p = perms["emp"][mrkv_prev][int(mrkv_now)]
+    unemp_p = perms["unemp"][mrkv_prev][int(mrkv_now)]
+    EmpNow = np.empty(employed.size)
+    EmpNow[employed] = rng.permutation(emp_p)
+    EmpNow[unemployed] = rng.permutation(unemp_p)
+    return EmpNow.astype(bool)
 
 
 def choice_cdf(P_row):
@@ -625,6 +682,7 @@ class KSModel:
         self.ss = steady_state(e)
         mk = make_MrkvArray(e)
         self.MrkvArray, self.MrkvIndArray = mk["MrkvArray"], mk["MrkvIndArray"]
+        self.MrkvEmplArray = mk["MrkvEmplArray"]
         self.econ_tauchen = mk["TauchenAux"]
         self.agent_tauchen = tauchen_for(a["LaborStatesNo"], a["LaborAR"], a["LaborSD"])   # Q5
         self.LSStates = labor_levels(self.agent_tauchen[0])
@@ -646,8 +704,10 @@ class KSModel:
         e = self.e
         T = act_T or e["act_T"]
         N = self.a["AgentCount"]
-        emp, lab = sim_birth_labor(N, self.a["LaborStatesNo"], e["UrateB"], seed=self.agent_seed,
-                                   Mrkv=e["MrkvNow_init"])
+        emp, lab, rng = sim_birth_labor(N, self.a["LaborStatesNo"], e["UrateB"], seed=self.agent_seed,
+                                        Mrkv=e["MrkvNow_init"], UrateG=e["UrateG"], return_rng=True)
+        ks = e["UrateB"] != 0.0 or e["UrateG"] != 0.0     # else everyone stays employed
+        perms = make_emp_idx_arrays(N, e["UrateB"], e["UrateG"], self.MrkvEmplArray, self.MrkvArray) if ks else None
         a_prev = np.full(N, self.ss["KSS"])
         sow = dict(Mnow=self.ss["MSS"], Aprev=self.ss["KSS"], Mrkv=0, Rnow=self.ss["RSS"], Wnow=self.ss["WSS"])
         hist = dict(Mrkv=[], Aprev=[], Mnow=[], Urate=[])
@@ -657,6 +717,8 @@ class KSModel:
             t1 = min(T, t0 + block)
             U = u_source(ge_iter, t0, t1)
             for t in range(t0, t1):
+                if ks:
+                    emp = employment_step(emp, sow["Mrkv"], e["UrateB"], perms, rng)
                 a_prev, lab, m_now, c_now = sim_one_period(a_prev, lab, emp, U[t - t0], sow["Rnow"], sow["Wnow"],
                                                            sow["Mnow"], sow["Mrkv"], self.LSStates, self.cdf_table,
                                                            m_tab, c_tab, self.Mgrid)
@@ -668,8 +730,8 @@ class KSModel:
                 hist["Mnow"].append(Mnow)
                 hist["Urate"].append(Urate)
                 if record:
-                    trace.append((a_prev.copy(), lab.copy()))
-        return dict(sow=sow, hist=hist, aNow=a_prev, lab=lab, trace=trace)
+                    trace.append((a_prev.copy(), lab.copy(), emp.copy()))
+        return dict(sow=sow, hist=hist, aNow=a_prev, lab=lab, emp=emp, trace=trace)
 
     def solve(self, u_source, max_loops=MAX_LOOPS, tol=MARKET_TOLERANCE, log=None):
         """[HARK 0.12] Market.solve (C5)."""

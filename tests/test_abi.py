@@ -54,13 +54,13 @@ def test_struct_layouts(lib):
     assert ctypes.sizeof(_lib.EgmDims) == 16
     assert ctypes.sizeof(_lib.EgmInputs) == 9 * 8
     assert ctypes.sizeof(_lib.Market) == 6 * 8
-    assert ctypes.sizeof(_lib.PanelModel) == 16 + 5 * 8 + 8   # + act_T (padded)
-    assert ctypes.sizeof(_lib.PanelBatch) == 24 + 5 * 8
+    assert ctypes.sizeof(_lib.PanelModel) == 16 + 5 * 8 + 8   # + act_T, unemployed
+    assert ctypes.sizeof(_lib.PanelBatch) == 24 + 5 * 8 + 8   # + unemployed (padded)
 
 
 def test_argument_validation_without_gpu(lib):
     from aiyagari_hark_amd import _lib
-    assert lib.aiy_version() == 200
+    assert lib.aiy_version() == 210
     # null handle -> AIY_ERR_ARG, nothing launched
     d = _lib.EgmDims(1, 28, 15, 32)
     i = _lib.EgmInputs()
@@ -96,10 +96,11 @@ def test_missing_library_fails_loudly(tmp_path):
 def test_panel_table_bytes_host_only(lib):
     """aiy_panel_table_bytes is pure host arithmetic: sizes grow with the grid, and
     unsupported shapes are refused with -1 before any device work."""
-    small = lib.aiy_panel_table_bytes(7, 15, 32)
-    big = lib.aiy_panel_table_bytes(7, 15, 10000)
+    small = lib.aiy_panel_table_bytes(7, 15, 32, 0)
+    big = lib.aiy_panel_table_bytes(7, 15, 10000, 0)
+    assert lib.aiy_panel_table_bytes(7, 15, 32, 1) > small     # + the unemployed cells
     assert 0 < small < big
     assert small % 256 == 0 and big % 256 == 0
-    assert lib.aiy_panel_table_bytes(7, 15, 1) == -1
-    assert lib.aiy_panel_table_bytes(0, 15, 32) == -1
-    assert lib.aiy_panel_table_bytes(17, 15, 32) == -1
+    assert lib.aiy_panel_table_bytes(7, 15, 1, 0) == -1
+    assert lib.aiy_panel_table_bytes(0, 15, 32, 0) == -1
+    assert lib.aiy_panel_table_bytes(17, 15, 32, 0) == -1

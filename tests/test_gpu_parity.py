@@ -431,7 +431,7 @@ def test_panel_tables_semantics(gpu, name):
     n_lab = S // 4
     h = _lib.handle(gpu.index)
     g = _tab_geom(n_lab, n_M, n_a)
-    assert h.lib.aiy_panel_table_bytes(n_lab, n_M, n_a) == g["bytes"]
+    assert h.lib.aiy_panel_table_bytes(n_lab, n_M, n_a, 0) == g["bytes"]
     tab = build_tables(h, torch.as_tensor(m[None]).to(gpu), torch.as_tensor(c[None]).to(gpu), n_lab, gpu)
     torch.cuda.synchronize()
     raw = tab[0].cpu().numpy()

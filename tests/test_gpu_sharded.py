@@ -97,7 +97,7 @@ def test_two_step_shards_equal_unsharded(gpu, mode):
                 keep.append(ut)
                 up = ut.data_ptr()
             h.check(h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), nl, off, _lib.ptr(p.a), _lib.ptr(p.lab), up,
-                                               seed, 1, t, _lib.ptr(p.sow), sp), "local")
+                                               None, seed, 1, t, _lib.ptr(p.sow), sp), "local")
         total = shards[0][2].sow[6] + shards[1][2].sow[6]
         for off, nl, p in shards:
             p.sow[6] = total
@@ -209,11 +209,11 @@ def test_run_past_history_is_refused(gpu):
     h = _lib.handle(gpu.index)
     pm, mk = p._model[0], p._model[1]
     rc = h.lib.aiy_sim_periods(h.h, ctypes.byref(pm), ctypes.byref(mk), N, 0, N, _lib.ptr(p.a), _lib.ptr(p.lab), None,
-                               0, 1, 0, 5, T - 4, _lib.ptr(p.sow), _lib.ptr(p.hist_A), _lib.ptr(p.hist_M),
+                               0, None, 0, 1, 0, 5, T - 4, _lib.ptr(p.sow), _lib.ptr(p.hist_A), _lib.ptr(p.hist_M),
                                _lib.stream_ptr())
     assert rc == -1 and b"act_T" in h.lib.aiy_last_error(h.h)
-    rc = h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), N, 0, _lib.ptr(p.a), _lib.ptr(p.lab), None, 0, 1, T,
-                                    _lib.ptr(p.sow), _lib.stream_ptr())
+    rc = h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), N, 0, _lib.ptr(p.a), _lib.ptr(p.lab), None, None, 0, 1,
+                                    T, _lib.ptr(p.sow), _lib.stream_ptr())
     assert rc == -1
     p.run(0, T, shock_mode="philox")   # the full history is fine
     torch.cuda.synchronize()

@@ -240,3 +240,34 @@ def test_fast_hist_step_equals_reference_step():
     a = ST.hist_step(mass, lo, wlo, P)
     b = ST.hist_step_fast(mass, lo, wlo, P)
     assert np.max(np.abs(a - b)) < 1e-16
+
+
+def test_employment_restatements_agree():
+    """Krusell-Smith employment (AS:1042-1156, 1173-1214, 1222-1240): the product's host
+    restatement (setup_math, drives the device panel) and the oracle's draw the same
+    employment, period by period, from the same agent RNG; counts are exact per macro
+    state; an AgentCount whose rounding breaks the counts raises."""
+    from aiyagari_hark_amd import setup_math as sm
+    p = dict(H.INIT_ECONOMY, UrateB=0.10, UrateG=0.04)
+    mk = H.make_MrkvArray(p)
+    E, A = mk["MrkvEmplArray"], mk["MrkvArray"]
+    N = 700
+    e1, l1, r1 = H.sim_birth_labor(N, 7, 0.10, seed=0, UrateG=0.04, return_rng=True)
+    e2, l2, r2 = sm.birth_states(N, 7, 0.10, seed=0, UrateG=0.04, with_rng=True)
+    np.testing.assert_array_equal(e1, e2)
+    np.testing.assert_array_equal(l1, l2)
+    perms = H.make_emp_idx_arrays(N, 0.10, 0.04, E, A)
+    trans = sm.employment_transitions(N, 0.10, 0.04, E, A)
+    hist = H.make_Mrkv_history(A, 300)
+    for t in range(300):
+        now = 0 if t == 0 else hist[t - 1]
+        e1 = H.employment_step(e1, now, 0.10, perms, r1)
+        e2 = sm.employment_step(e2, now, 0.10, trans, r2)
+        np.testing.assert_array_equal(e1, e2)
+        assert int((~e1).sum()) == (70 if now == 0 else 28)
+    bad = 707   # round(0.04 * 707) etc. do not balance the flows
+    tb = sm.employment_transitions(bad, 0.10, 0.04, E, A)
+    eb, _, rb = sm.birth_states(bad, 7, 0.10, with_rng=True, UrateG=0.04)
+    with pytest.raises(ValueError):
+        for t in range(50):
+            eb = sm.employment_step(eb, t % 2, 0.10, tb, rb)
