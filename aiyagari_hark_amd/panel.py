@@ -60,7 +60,7 @@ class DevicePanel:
     def reset(self, a0, lab0, Mnow, Aprev, Mrkv, Rnow, Wnow):
         """sim_birth + Market.reset sow_init (Aiyagari_Support.py:1621-1628)."""
         a0 = np.broadcast_to(np.asarray(a0, dtype=np.float64), (self.n_local,))
-        self.a.copy_(torch.from_numpy(np.ascontiguousarray(a0)))
+        self.a.copy_(torch.from_numpy(np.array(a0, dtype=np.float64, order="C")))
         self.lab.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(lab0, dtype=np.uint8))))
         sow = np.zeros(_lib.AIY_SOW_DOUBLES)
         sow[:6] = [Mnow, Aprev, Mrkv, Rnow, Wnow, 0.0]
@@ -264,7 +264,7 @@ class BatchedPanel:
         (Mnow, Aprev, Mrkv, Rnow, Wnow)."""
         a0 = np.asarray(a0, dtype=np.float64)
         a0 = np.broadcast_to(a0[:, None] if a0.ndim == 1 else a0, (self.n_cal, self.n_agents))
-        self.a.copy_(torch.from_numpy(np.ascontiguousarray(a0)))
+        self.a.copy_(torch.from_numpy(np.array(a0, dtype=np.float64, order="C")))
         self.lab.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(lab0, dtype=np.uint8))))
         sow = np.zeros((self.n_cal, _lib.AIY_SOW_DOUBLES))
         sow[:, :5] = np.asarray(sow0, dtype=np.float64)

@@ -170,7 +170,8 @@ def table2_leg(args, world, rank, dev):
                evaluations_rank0=per_rank[0]["evaluations"], r_percent=[round(100 * x, 6) for x in r],
                saving_rate_percent=[round(100 * 0.08 * x, 5) for x in kty])
     log(f"[bench] table2: {el / args.steps:.3f} s per sweep ({out['value']:.2f} GE solves/s); "
-        f"hist kernel {hist_ms / args.steps:.1f} ms per sweep, {hist_gbs:.0f} GB/s algorithmic")
+        f"hist kernel {hist_ms / args.steps:.1f} ms per sweep, {hist_gbs:.0f} GB/s algorithmic; "
+        f"hist_point_iters={point_iters} hist_launches={hist_n}")
     return out
 
 

@@ -1,6 +1,10 @@
 """Summarise rocprofv3 PMC passes into per-launch HBM traffic for bench.py.
 
-Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json>
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [bench_log]
+
+With the log of the profiled bench run (its "hist_point_iters=" line), the device-resident
+histogram also gets hbm_bytes_per_point_iter: its launches differ in iteration count, so
+bench.py scales the per-(state, node)-point-iteration traffic to its own launches.
 
 FETCH_SIZE and WRITE_SIZE (KB) come from separate rocprofv3 --pmc passes (they do not
 fit one pass on gfx950).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the
@@ -29,8 +33,19 @@ def per_kernel(d, counter):
     return {k: (tot[k] / len(disp[k]), len(disp[k])) for k in tot}
 
 
+def point_iters(log_path):
+    import re
+    n = 0
+    for line in open(log_path, errors="replace"):
+        m = re.search(r"hist_point_iters=(\d+)", line)
+        if m:
+            n += int(m.group(1))
+    return n
+
+
 def main():
     fd, wd, out = sys.argv[1:4]
+    pts = point_iters(sys.argv[4]) if len(sys.argv) > 4 else 0
     fetch = per_kernel(fd, "FETCH_SIZE")
     write = per_kernel(wd, "WRITE_SIZE")
     res = {}
@@ -41,6 +56,9 @@ def main():
         res[short] = dict(kernel=k, fetch_kb_raw=f_kb, write_kb=w_kb, dispatches=[nf, nw],
                           hbm_bytes_per_launch=(2.0 * f_kb + w_kb) * 1024.0,
                           correction="FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1")
+        if short == "hist_cluster_kernel" and pts > 0:
+            res[short]["point_iters"] = pts
+            res[short]["hbm_bytes_per_point_iter"] = (2.0 * f_kb * nf + w_kb * nw) * 1024.0 / pts
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         print(f"{k}: {v['hbm_bytes_per_launch'] / 1e6:.2f} MB/launch (fetch raw {v['fetch_kb_raw']:.0f} KB, "
