@@ -20,8 +20,9 @@ struct aiy_handle {
   unsigned long long* d_dist = nullptr;
   int* d_last = nullptr;
   size_t egm_cap = 0;
-  int* d_egm_idx = nullptr;          // [2][rows][kIdxRow] search index of the ping-pong tables
-  size_t egm_idx_cap = 0;            // ints
+  int* d_egm_hint = nullptr;         // EGM row hints [work item][rows x S] (egm.hip)
+  size_t egm_hint_cap = 0;           // ints
+  unsigned long long egm_hint_sig = ~0ull;   // shape the hints belong to
   // host pinned mirrors
   unsigned long long* h_dist = nullptr;
   int* h_last = nullptr;

@@ -202,7 +202,8 @@ def reset_rule(econ, agent):
 
 def egm_kernel_time(agent, n_launch=20):
     """Average duration of one EGM cycle kernel from the converged policy (HIP events on
-    its stream, aiy_egm_kernel_time; the search-index build is outside)."""
+    its stream, aiy_egm_kernel_time; its row hints set by one untimed launch, as the
+    cycle before sets them in a solve)."""
     import torch
     from aiyagari_hark_amd import _lib
     sol = agent.solution[0]

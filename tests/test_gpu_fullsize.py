@@ -48,14 +48,18 @@ def solved(big, gpu):
 def test_egm_step_10k_bit_exact(big, gpu):
     from aiyagari_hark_amd.egm import EgmBatch, egm_step
     m, (Rk, Wk, Mk), args = big
-    mt, ct = H.egm_step(None, None, *args)
-    mt, ct = H.egm_step(mt, ct, *args)
-    m3, c3 = H.egm_step(mt, ct, *args)
+    m1, c1 = H.egm_step(None, None, *args)
+    m2, c2 = H.egm_step(m1, c1, *args)
+    m3, c3 = H.egm_step(m2, c2, *args)
     lab = np.array([m.LSStates[s // 4] for s in range(28)])
     b = EgmBatch.from_numpy(m.aGrid, m.Mgrid, m.MrkvIndArray, Rk, Wk, Mk, lab, 0.96, 1.0, device=gpu)
-    om, oc = egm_step(b, torch.as_tensor(mt[None]).to(gpu), torch.as_tensor(ct[None]).to(gpu))
-    assert np.array_equal(oc[0].cpu().numpy(), c3)
-    assert np.array_equal(om[0].cpu().numpy(), m3)
+    dev = lambda x: torch.as_tensor(x[None]).to(gpu)
+    # no row hints yet (global searches), then hints from the cycle before (as in a
+    # solve), then hints from the same tables (the window path everywhere)
+    for tables, (wm, wc) in (((m1, c1), (m2, c2)), ((m2, c2), (m3, c3)), ((m2, c2), (m3, c3))):
+        om, oc = egm_step(b, dev(tables[0]), dev(tables[1]))
+        assert np.array_equal(oc[0].cpu().numpy(), wc)
+        assert np.array_equal(om[0].cpu().numpy(), wm)
 
 
 @pytest.mark.timeout(600)

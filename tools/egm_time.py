@@ -33,8 +33,19 @@ def child(lib):
     _, _, cyc, _ = egm_solve(b)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
+    import ctypes
+    from aiyagari_hark_amd import _lib
+    mt, ct, _, _ = egm_solve(b)
+    m0, c0 = mt.contiguous(), ct.contiguous()
+    mo, co = torch.empty_like(m0), torch.empty_like(c0)
+    d, i = b._abi()
+    h = _lib.handle(0)
+    ms = ctypes.c_float()
+    n = 50
+    h.check(h.lib.aiy_egm_kernel_time(h.h, ctypes.byref(d), ctypes.byref(i), _lib.ptr(m0), _lib.ptr(c0), _lib.ptr(mo),
+                                      _lib.ptr(co), n, ctypes.byref(ms), torch.cuda.current_stream().cuda_stream), "t")
     print(json.dumps(dict(lib=os.path.basename(lib), cycles=int(cyc[0]), solve_s=dt,
-                          us_per_cycle=1e6 * dt / int(cyc[0]))), flush=True)
+                          us_per_cycle=1e6 * dt / int(cyc[0]), kernel_us=1e3 * ms.value / n)), flush=True)
 
 
 if __name__ == "__main__":
