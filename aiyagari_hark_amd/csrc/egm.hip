@@ -50,8 +50,8 @@ constexpr int kEgmBlock = 256;
 #ifndef AIY_EGM_ORDER
 #define AIY_EGM_ORDER 0
 #endif
-// Diagnostic builds (tools/egm_time.py): 1 = trivial phase 1, 2 = trivial phase 2,
-// 4 = window path only.  Never the product build.
+// Diagnostic builds (tools/egm_time.py, tools/egm_stamps.py): 1 = trivial phase 1,
+// 2 = trivial phase 2, 8 = per-wave clock stamps.  Never the product build.
 #ifndef AIY_EGM_DIAG
 #define AIY_EGM_DIAG 0
 #endif
@@ -72,6 +72,25 @@ constexpr int kSlots = 3 * kSub + 4;
 constexpr int kWin = 2 * kWave;
 
 constexpr int kHintBack = 8;
+
+#if AIY_EGM_DIAG == 8
+constexpr int kStampWaves = 1 << 16;
+constexpr int kStamps = 6;
+__device__ unsigned long long g_egm_stamps[kStampWaves * kStamps];
+#define AIY_EGM_STAMP(W, k)                                                                        \
+  do {                                                                                            \
+    const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                                \
+    const unsigned long long _c = __builtin_amdgcn_s_memtime();                                    \
+    const int _slot = (W).w * kEgmWaves + (int)(threadIdx.x / kWave);                              \
+    if ((threadIdx.x & (kWave - 1)) == 0 && _slot < kStampWaves) {                                 \
+      g_egm_stamps[_slot * kStamps + (k)] = (k) == 0 ? _t : _c;                                    \
+    }                                                                                             \
+  } while (0)
+#else
+#define AIY_EGM_STAMP(W, k) \
+  do {                     \
+  } while (0)
+#endif
 
 struct EgmDev {
   int n_cal, S, n_M, n_a;
@@ -172,15 +191,18 @@ __device__ __forceinline__ void load_win(const double* __restrict__ xr, const do
   // branch-free and untouched until use (every lane loads, indices clamped into the
   // row; nodes past x[n] are masked when the window is written to LDS): a window load
   // is never behind a branch or an early use, so its wait can count the loads issued
-  // after it
+  // after it.  32-bit unsigned offsets from the wave-uniform row pointer.
   C.base = base;
-  const int b = base < 0 ? 0 : base;
-  const int t0 = b + lane, t1 = t0 + kWave;
-  const int u0 = t0 <= n ? t0 : n, u1 = t1 <= n ? t1 : n;
-  C.x0 = xr[u0];
-  C.y0 = yr[u0];
-  C.x1 = xr[u1];
-  C.y1 = yr[u1];
+  const unsigned b = base < 0 ? 0u : (unsigned)base;
+  const unsigned t0 = b + (unsigned)lane, t1 = t0 + kWave;
+  const unsigned un = (unsigned)n;
+  const unsigned u0 = t0 <= un ? t0 : un, u1 = t1 <= un ? t1 : un;
+  // byte offsets as 32-bit values: global_load with the SGPR row base + a VGPR offset
+  const unsigned o0 = u0 << 3, o1 = u1 << 3;
+  C.x0 = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(xr) + o0);
+  C.y0 = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(yr) + o0);
+  C.x1 = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(xr) + o1);
+  C.y1 = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(yr) + o1);
 }
 
 // Window start from the hint (the lower bound of the tile's first query in this row
@@ -194,18 +216,16 @@ __device__ __forceinline__ int win_base(int hint, int n1) {
 }
 
 // HARK 0.12 LinearInterp of a row (n + 1 nodes, bracket i = max(searchsorted(x[:-1], q),
-// 1), NaN below x[0]) at the lane's query q, wave-cooperatively from the staged window:
-// the window goes to the wave's LDS slice (X, Y), every lane finds its lower bound by a
-// 7-step branch-free search in LDS and reads its bracket there.  ok: the window holds
-// the lane's bracket (no NaN node, hint not stale); lanes without it are redone from
-// global memory (interp_row_global) -- the same lower bound, so the result never depends
-// on the hint.  lb: the lane's lower bound.
-__device__ __forceinline__ double interp_win(const RowWin& C, int n, double q, double* X, double* Y, int lane,
-                                             int& lb, bool& ok) {
-  const int base = C.base;
-  ok = false;
-  lb = 0;
-  if (base < 0) return 0.0;   // no hint for this row yet (wave-uniform)
+// 1), NaN below x[0]) at the lane's query q, wave-cooperatively from a staged window, in
+// two steps so a wave can run two rows' searches side by side:
+//   stage_win:  the window into the wave's LDS slice (X, Y); true where a node is NaN;
+//   search_win: (after a wave fence) the lane's lower bound by a 7-step branch-free
+//               search in LDS, the bracket from LDS, the interpolated value.
+// ok: the window holds the lane's bracket (a hint, no NaN node, not stale); lanes without
+// it are redone from global memory (interp_row_global) -- the same lower bound, so the
+// result never depends on the hint.  lb: the lane's lower bound.
+__device__ __forceinline__ bool stage_win(const RowWin& C, int n, double* X, double* Y, int lane) {
+  const int base = C.base < 0 ? 0 : C.base;
   const double inf = __builtin_inf();
   const double x0 = base + lane <= n ? C.x0 : inf;
   const double x1 = base + lane + kWave <= n ? C.x1 : inf;
@@ -213,13 +233,19 @@ __device__ __forceinline__ double interp_win(const RowWin& C, int n, double q, d
   X[lane + kWave] = x1;
   Y[lane] = C.y0;
   Y[lane + kWave] = C.y1;
-  const bool nan_nodes = __any((x0 != x0) || (x1 != x1));
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return (x0 != x0) || (x1 != x1);
+}
+
+__device__ __forceinline__ double search_win(int hint_base, bool nan_nodes, int n, double q, const double* X,
+                                             const double* Y, int& lb, bool& ok) {
+  const int base = hint_base < 0 ? 0 : hint_base;
+  const double inf = __builtin_inf();
   const int L = n - base < kWin ? n - base : kWin;   // searchable nodes (x[:-1]) in the window
-  const double xf = X[0];
-  ok = !nan_nodes && (base == 0 || xf < q) && (base + kWin - 1 >= n || q <= X[kWin - 1]);
+  const double xf = X[0], xlast = X[kWin - 1];
+  // no short-circuit: a branch here would keep two rows' searches from interleaving
+  const bool lo_ok = (base == 0) | (xf < q);
+  const bool hi_ok = (base + kWin - 1 >= n) | (q <= xlast);
+  ok = (hint_base >= 0) & !nan_nodes & lo_ok & hi_ok;
   // branch-free search over the whole window (nodes past x[n] are +inf); counting x[n]
   // too is undone by the clamp to L (lower_bound over x[:-1], sorted rows)
   int pos = 0;
@@ -308,7 +334,9 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
     }
     return;
   } else {
-    const size_t tab_cal = (size_t)cal * S * n_M * n1;
+    // calibration base pointers once; rows by 32-bit offsets (S n_M (n_a + 1) < 2^31)
+    const double* __restrict__ mcal = m_next + (size_t)cal * S * n_M * n1;
+    const double* __restrict__ ccal = c_next + (size_t)cal * S * n_M * n1;
     const int n_sp = (S - wave + kEgmWaves - 1) / kEgmWaves;
     const int nrr = n_sp * ROWS;
     auto row_of = [&](int rr, int& sp, int& r) {
@@ -317,15 +345,15 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
     };
     auto row_off = [&](int sp, int r) {
       const int jr = ROWS == 2 ? st.j[sp] - 1 + r : 0;
-      return tab_cal + ((size_t)sp * n_M + jr) * n1;
+      return (unsigned)((sp * n_M + jr) * n1);
     };
     // unconditional (rows past the wave's last repeat it): every fetch issues the same
     // four loads, so the number of loads issued after a window is static
     auto fetch = [&](int rr, RowWin& w) {
       int sp2, r2;
       row_of(rr < nrr ? rr : nrr - 1, sp2, r2);
-      const size_t off2 = row_off(sp2, r2);
-      load_win(m_next + off2, c_next + off2, n, win_base(st.hint[ROWS * sp2 + r2], n1), lane, w);
+      const unsigned off2 = row_off(sp2, r2);
+      load_win(mcal + off2, ccal + off2, n, win_base(st.hint[ROWS * sp2 + r2], n1), lane, w);
     };
     // the V of next state s' from its rows' values (c_{s'} at M' by LinearInterpOnInterp1D)
     auto put_v = [&](int sp, double f0, double f1) {
@@ -341,33 +369,55 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
     // memory, after the loop -- so the loop body has no divergent global access and the
     // wait for each window counts exactly the loads issued after it
     unsigned redo = 0u;
-    auto step = [&](int rr, const RowWin& cur, double& f0) {
-      if (rr >= nrr) return;
-      int sp, r;
-      row_of(rr, sp, r);
-      const double q = st.R[sp] * a + st.Wl[sp];   // mNextArray (AS:1024)
-      int lb;
-      bool ok;
-      const double f = interp_win(cur, n, q, X, Y, lane, lb, ok);
-      if (__any(!ok)) redo |= 1u << (rr / ROWS);
-      st.hint[ROWS * sp + r] = __builtin_amdgcn_readfirstlane(lb);   // next cycle's hint (lane 0's bound)
-      if (ROWS == 2 && r == 0) f0 = f;
-      else put_v(sp, f0, f);
+    // one unit = rows 2u and 2u + 1 (the two M' rows of one s', or two s' when n_M = 1),
+    // staged to the wave's two LDS slices and searched side by side
+    double* XB = X + 2 * kWin;
+    double* YB = Y + 2 * kWin;
+    auto step_unit = [&](int u, const RowWin& wa, const RowWin& wb) {
+      const int ra = 2 * u, rb = 2 * u + 1;
+      if (ra >= nrr) return;   // wave-uniform
+      const bool has_b = rb < nrr;
+      int spa, pa, spb, pb;
+      row_of(ra, spa, pa);
+      row_of(has_b ? rb : ra, spb, pb);
+      const bool na = __any(stage_win(wa, n, X, Y, lane));
+      const bool nb = __any(stage_win(wb, n, XB, YB, lane));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double qa = st.R[spa] * a + st.Wl[spa];   // mNextArray (AS:1024)
+      const double qb = ROWS == 2 ? qa : st.R[spb] * a + st.Wl[spb];
+      int lba, lbb;
+      bool oka, okb;
+      const double fa = search_win(wa.base, na, n, qa, X, Y, lba, oka);
+      const double fb = search_win(wb.base, nb, n, qb, XB, YB, lbb, okb);
+      st.hint[ROWS * spa + pa] = __builtin_amdgcn_readfirstlane(lba);   // next cycle's hints (lane 0)
+      if (has_b) st.hint[ROWS * spb + pb] = __builtin_amdgcn_readfirstlane(lbb);
+      if (ROWS == 2) {
+        if (__any(!oka || !okb)) redo |= 1u << u;
+        put_v(spa, fa, fb);
+      } else {
+        if (__any(!oka)) redo |= 1u << ra;
+        put_v(spa, 0.0, fa);
+        if (has_b) {
+          if (__any(!okb)) redo |= 1u << rb;
+          put_v(spb, 0.0, fb);
+        }
+      }
     };
-    // windows of three rows in flight, in three fixed register sets (a rotation by copy
-    // would wait for the loads it copies)
-    RowWin w0, w1, w2;
-    fetch(0, w0);
-    fetch(1, w1);
-    double f0 = 0.0;
+    // two units' windows in flight, in two fixed register sets (a rotation by copy would
+    // wait for the loads it copies)
+    RowWin a0, b0, a1, b1;
+    fetch(0, a0);
+    fetch(1, b0);
 #pragma unroll 1
-    for (int rr = 0; rr < nrr; rr += 3) {
-      fetch(rr + 2, w2);
-      step(rr, w0, f0);
-      fetch(rr + 3, w0);
-      step(rr + 1, w1, f0);
-      fetch(rr + 4, w1);
-      step(rr + 2, w2, f0);
+    for (int u = 0; 2 * u < nrr; u += 2) {
+      fetch(2 * u + 2, a1);
+      fetch(2 * u + 3, b1);
+      step_unit(u, a0, b0);
+      fetch(2 * u + 4, a0);
+      fetch(2 * u + 5, b0);
+      step_unit(u + 1, a1, b1);
     }
 #pragma unroll 1
     while (redo != 0u) {   // wave-uniform
@@ -377,9 +427,9 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
       const double q = st.R[sp] * a + st.Wl[sp];
       double f[ROWS];
       for (int r = 0; r < ROWS; ++r) {
-        const size_t off = row_off(sp, r);
+        const unsigned off = row_off(sp, r);
         int lb;
-        f[r] = interp_row_global(m_next + off, c_next + off, n, q, lb);
+        f[r] = interp_row_global(mcal + off, ccal + off, n, q, lb);
         st.hint[ROWS * sp + r] = __builtin_amdgcn_readfirstlane(lb);
       }
       put_v(sp, f[0], f[ROWS - 1]);
@@ -451,12 +501,14 @@ __device__ __forceinline__ double egm_phase2(const EgmDev& A, const double* __re
 // for cycle n+1.  Nothing is written after convergence, so slot (last % 3) keeps the
 // final distance for the host.
 template <int SMAX, int SC, bool TERMINAL, int ROWS>
-__global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) void egm_cycle_kernel(
+__global__ __launch_bounds__(kEgmBlock, (SC > 0 || SMAX <= 16) ? AIY_EGM_WAVES_PER_EU : (SMAX <= 32 ? 3 : 1)) void egm_cycle_kernel(
     EgmDev A, const double* __restrict__ m_next, const double* __restrict__ c_next, double* __restrict__ m_out,
     double* __restrict__ c_out, int* __restrict__ hints, int n_tiles, int n_work, int cycle,
     unsigned long long* dist_slots, int* last_cycle, double tol) {
   const EgmWork W = egm_work(n_tiles, A.n_M);
   if (W.w >= n_work) return;   // grid padding (block-uniform)
+  AIY_EGM_STAMP(W, 0);
+  AIY_EGM_STAMP(W, 1);
   const int cal = W.cal;
   const bool lead = W.tile == 0 && W.k == 0;
   if (dist_slots != nullptr && cycle >= 3) {
@@ -477,16 +529,32 @@ __global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) v
     __syncthreads();
     if (s_skip) return;
   }
-  __shared__ double Vs[SMAX * kTile];
-  __shared__ double Pl[SMAX * SMAX];
-  __shared__ double s_win[kEgmWaves][2 * kWin];
+  constexpr int VN = SC > 0 ? SC : SMAX;   // LDS sized by the exact state count when known
+  __shared__ double Vs[VN * kTile];
+  __shared__ double Pl[VN * VN];
+  __shared__ double s_win[kEgmWaves][4 * kWin];
   __shared__ double s_al[SMAX], s_R[SMAX], s_Wl[SMAX], s_par[2];
   __shared__ int s_j[SMAX];
   __shared__ int s_hint[2 * SMAX];
   {
     const int S = SC > 0 ? SC : A.S;
     const double* Pc = A.P + (size_t)cal * S * S;
-    for (int q = threadIdx.x; q < S * S; q += kEgmBlock) Pl[q] = Pc[q];
+    if constexpr (SC > 0) {   // all loads in flight before the first LDS store
+      constexpr int NP = (SC * SC + kEgmBlock - 1) / kEgmBlock;
+      double pv[NP];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int q = threadIdx.x + u * kEgmBlock;
+        pv[u] = q < SC * SC ? Pc[q] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int q = threadIdx.x + u * kEgmBlock;
+        if (q < SC * SC) Pl[q] = pv[u];
+      }
+    } else {
+      for (int q = threadIdx.x; q < S * S; q += kEgmBlock) Pl[q] = Pc[q];
+    }
   }
   const EgmStage st{s_par, s_R, s_Wl, s_al, s_j, s_hint};
   egm_prologue<SC, TERMINAL, ROWS>(A, hints, W, st);
@@ -498,8 +566,9 @@ __global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) v
   const double a = A.a_grid[(size_t)cal * A.n_a + ic];
   const bool track = (dist_slots != nullptr) && cycle >= 2;
   __syncthreads();
+  AIY_EGM_STAMP(W, 2);
   const bool log_util = s_par[0] == 1.0;   // block-uniform: one of two straight-line bodies
-  double* X = s_win[wave];
+  double* X = s_win[wave];   // slices: X | Y | XB | YB
   double* Y = X + kWin;
 #if AIY_EGM_DIAG == 1
   for (int sp = wave; sp < A.S; sp += kEgmWaves) Vs[sp * kTile + (threadIdx.x & (kWave - 1))] = a + sp;
@@ -509,8 +578,10 @@ __global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) v
     egm_phase1<SC, TERMINAL, true, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
   else
     egm_phase1<SC, TERMINAL, false, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
+  AIY_EGM_STAMP(W, 3);
   __syncthreads();
   if (!TERMINAL && (int)threadIdx.x < ROWS * A.S) hints[(size_t)W.w * ROWS * A.S + threadIdx.x] = s_hint[threadIdx.x];
+  AIY_EGM_STAMP(W, 4);
   double dmax;
 #if AIY_EGM_DIAG == 2
   {
@@ -524,6 +595,7 @@ __global__ __launch_bounds__(kEgmBlock, SMAX <= 32 ? AIY_EGM_WAVES_PER_EU : 1) v
   if (log_util) dmax = egm_phase2<SMAX, SC, true>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
   else dmax = egm_phase2<SMAX, SC, false>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
 
+  AIY_EGM_STAMP(W, 5);
   if (dist_slots != nullptr) {
     if (track) {
       __shared__ double red[kEgmWaves];
@@ -587,6 +659,8 @@ static int32_t check_egm(aiy_handle* h, const aiy_egm_dims* d, const aiy_egm_inp
     return fail(h, AIY_ERR_ARG, "bad dims n_cal=%d S=%d n_M=%d n_a=%d", d->n_cal, d->S, d->n_M, d->n_a);
   if (d->S > AIY_MAX_STATES) return fail(h, AIY_ERR_UNSUPPORTED, "S=%d exceeds %d", d->S, AIY_MAX_STATES);
   if (d->n_cal > 65535 || d->n_M > 65535) return fail(h, AIY_ERR_UNSUPPORTED, "grid too large");
+  if ((long long)d->S * d->n_M * (d->n_a + 1) >= 2147483647LL)   // 32-bit row offsets per calibration
+    return fail(h, AIY_ERR_UNSUPPORTED, "policy table of one calibration exceeds 2^31 nodes");
   if (!in->a_grid || !in->P || !in->R_next || !in->W_next || !in->lab || !in->beta || !in->crra)
     return fail(h, AIY_ERR_ARG, "null input array");
   if (d->n_M > 1 && (!in->M_grid || !in->M_next)) return fail(h, AIY_ERR_ARG, "null M_grid/M_next");
@@ -801,6 +875,17 @@ extern "C" int32_t aiy_policy_eval(aiy_handle* h, int32_t S, int32_t n_M, int32_
 // Timing hook for bench.py: n_launch launches of the EGM cycle kernel on `stream`, each
 // bracketed by HIP events, after one untimed launch that sets the row hints (as every
 // cycle of a solve after the first finds them set by the cycle before).  BLOCKING.
+#if AIY_EGM_DIAG == 8
+// Diagnostic build only: the per-wave stamps of the last cycle launch ([w * 4 + wave][6]:
+// realtime at start, then shader clocks at start / after the prologue / after phase 1 /
+// after the phase barrier / at the end).
+extern "C" int32_t aiy_egm_diag_stamps(unsigned long long* host, int32_t n) {
+  if (n > kStampWaves * kStamps) n = kStampWaves * kStamps;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_egm_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int32_t aiy_egm_kernel_time(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in,
                                        const double* m_next, const double* c_next, double* m_out, double* c_out,
                                        int32_t n_launch, float* ms_out, aiy_stream stream) {
