@@ -46,7 +46,7 @@ def child(lib, opts):
         sys.path.insert(0, ROOT)
         import bench
         econ, agent = bench.make_economy(seed=0, n_agents=N, n_a=n_a, act_T=2000, device=dev, t_discard=500)
-        bench.run_step(econ, agent, bench.Probe())
+        econ.solve()
         bench_panel = agent.panel
     for (res, agents, order, presort, Tt) in opts:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res), "opt")
