@@ -34,6 +34,7 @@ AIY_OPT_RESIDENT_STREAM = 5
 AIY_OPT_HIST_RESIDENT = 6
 AIY_OPT_HIST_CLUSTER = 7
 AIY_OPT_HIST_ACCEL = 8
+AIY_OPT_HIST_KRYLOV = 9
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

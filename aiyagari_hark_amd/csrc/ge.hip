@@ -169,7 +169,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   std::vector<double> dist(n_cal);
   aiy_egm_dims dims{n_cal, S, 1, n_a};
   aiy_egm_inputs in{M->a_grid, Mg, M->P, Rn, Wn, Mn, M->lab, M->beta, M->crra};
-  const int saved_accel = h->hist_accel;
+  const int saved_accel = h->hist_accel, saved_krylov = h->hist_krylov;
   int steps = 0;
   int32_t rc = AIY_OK;
   long long cyc_sum = 0, it_sum = 0;
@@ -202,10 +202,12 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
                          1.0 / ((double)S * n_a));
       AIY_CHECK_LAUNCH(h);
     }
-    h->hist_accel = o->accel;
+    h->hist_accel = o->accel > 0 ? o->accel : 0;   // accel < 0: BiCGSTAB (AIY_OPT_HIST_KRYLOV)
+    h->hist_krylov = o->accel < 0;
     rc = aiy_hist_solve(h, n_cal, S, n_a, lo, wlo, M->P, M->a_grid, o->hist_tol,
                         o->max_hist_iter > 0 ? o->max_hist_iter : 200000, 64, mass, hw, Ks.data(), its.data(), stream);
     h->hist_accel = saved_accel;
+    h->hist_krylov = saved_krylov;
     if (rc) break;
     for (int c = 0; c < n_cal; ++c) {
       cyc_sum += cyc[c];
@@ -215,6 +217,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     ++steps;
   }
   h->hist_accel = saved_accel;
+  h->hist_krylov = saved_krylov;
   if (rc) return rc;
   for (int c = 0; c < n_cal; ++c) {
     const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];

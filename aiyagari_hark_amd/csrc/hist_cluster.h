@@ -1,0 +1,106 @@
+// Shared pieces of the device-resident distribution-iteration kernels (hist_resident.hip:
+// plain / Aitken iteration; hist_krylov.hip: BiCGSTAB): the per-calibration cluster run
+// description, the covering-span record, the cluster barrier and wave sums.
+#pragma once
+
+#include "common.h"
+
+namespace aiy {
+
+constexpr int kHcMaxG = 128;                       // workgroups per calibration cluster
+constexpr int kHcCand = 32;                        // covering workgroups per (row, workgroup)
+constexpr int kHcRows = 8;                         // rows whose push loads are in flight together
+// rows whose gather loads are in flight together: all (S <= 8) for one column per thread
+template <int SMAX, int KC, int TH>
+struct HcGather {
+  static constexpr int kRows = SMAX == 8 ? 8 : 4;
+};
+constexpr size_t kHcLdsTotal = 160 * 1024;         // per CU
+constexpr unsigned long long kHcTimeoutTicks = 200000000ull;   // 2 s of the 100 MHz clock
+constexpr int kHcCtrStride = 32;
+constexpr int kHcRedRec = 8;                      // doubles per (parity, workgroup) record of `dist`                   // uints between cluster counters (128 B)
+
+struct HcRun {
+  int n_cal, cal0, S, n_a, G, nj, cap;   // cap: doubles of the span buffer / one slab
+  const int* lo;          // [n_cal][S][n_a]
+  const double* wlo;      // [n_cal][S][n_a]
+  const double* P;        // [n_cal][S][S]
+  double* mass;           // [n_cal][S][n_a] in: start, out: final
+  double* slab;           // [launch cals][G][2][cap]
+  int* span;              // [launch cals][G][SMAX][4] (first, len, left base, right base)
+  unsigned* ctr;          // [launch cals][kHcCtrStride]
+  double* dist;           // [launch cals][2][G][4]: sup-norm change, Aitken dot products, valid
+  double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0)
+  int accel;              // Aitken extrapolation period E (0: plain iteration = the oracle's)
+  int* iters_out;         // [n_cal]
+  unsigned* err;          // 0 ok, 1 timeout, 2 span overflow / not monotone, 3 candidate overflow
+  double tol;
+  int max_iter;
+};
+
+struct HcCand {
+  int w, first, len, base;   // destination d of the covering span sits at slab/LDS index base + d
+};
+
+// Cluster barrier: lane 0 adds one to the cluster counter (after the caller's drained sc1
+// stores) and waits until it reaches `target`.  False on timeout (error word set).
+__device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsigned target, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+        __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *s_flag = ok;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// One covering span's value at destination d: the own span from LDS (read once by the
+// column's owner, then re-zeroed for the next push), a foreign one from its published slab.
+__device__ __forceinline__ double hc_take(const HcCand& c, int w, int d, int par, int cap, const double* slab_cl,
+                                          double* Tacc) {
+  const int q = c.base + d;
+  // two destinations (added at the use): one shared register would make the LDS read
+  // wait for every earlier slab load in flight (write-after-write on the register)
+  double vg = 0.0, vl = 0.0;
+  if (c.w == w) {
+    vl = Tacc[q];
+    Tacc[q] = 0.0;
+  } else {
+    vg = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + q]);
+  }
+  return vg + vl;
+}
+
+// Sum over the 64 lanes (DPP: row shifts, then row broadcasts), valid in lane 63.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_add_src(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_sum_lane63(double v) {
+  v += dpp_add_src<0x111, 0xF>(v);   // row_shr:1
+  v += dpp_add_src<0x112, 0xF>(v);   // row_shr:2
+  v += dpp_add_src<0x114, 0xF>(v);   // row_shr:4
+  v += dpp_add_src<0x118, 0xF>(v);   // row_shr:8   (lane 15 of every row: the row's sum)
+  v += dpp_add_src<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_add_src<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+  return v;
+}
+
+// BiCGSTAB form of the cluster kernel (hist_krylov.hip) for (S, padded S, columns per
+// thread) and its state count (*smax_k); nullptr when there is no instantiation
+const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k);
+
+}  // namespace aiy

@@ -1,0 +1,630 @@
+// Device-resident stationary distribution by BiCGSTAB (build-defined row E2, Krylov mode).
+//
+// The distribution iteration mass' = T mass (Young lottery push, then the income mix;
+// hist_resident.hip) converges at the rate of T's second eigenvalue.  For the Table II
+// cells near r = 1/beta - 1 T has a dense cluster of eigenvalues just below 1 (rho = 0,
+// sigma = 0.2, CRRA = 1: 0.99916, 0.99859, 0.99801, ...), so the plain iteration needs
+// ~16 000 sweeps from the uniform start and single-mode Aitken extrapolation removes only
+// one of those modes.  Here each calibration's cluster solves (I - T) x = 0 by BiCGSTAB
+// (van der Vorst 1992) started from the given mass: every Krylov step is one matvec T q
+// with exactly the cluster machinery of the plain kernel (push into LDS spans, publish
+// the foreign parts write-through, cluster barrier, gather, mix), plus cluster-wide dot
+// products carried on a light barrier.  Measured on the CPU restatement (scratch study,
+// DESIGN.md §4b): 1 066 matvecs instead of 15 828 plain sweeps cold, 602 instead of
+// 10 199 warm.
+//
+//   restart:  r = T x - x;  rho = <rh, r>;  stop if max|r| < tol (mass = T x)
+//             p = r
+//   loop:     v = p - T p;                   alpha = rho / <rh, v>   (max|r| checked here)
+//             s = r - alpha v;  t = s - T s; omega = <t, s> / <t, t>
+//             x += alpha p + omega s;  r = s - omega t
+//             rho' = <rh, s> - omega <rh, t>;  beta = (rho' / rho) (alpha / omega)
+//             p = r + beta (p - omega v)
+//   when the recursive residual is below tol (or a scalar breaks down) the true residual
+//   is formed again (restart), so the returned mass is T x for an x with
+//   max|T x - x| < tol: the stopping rule of oracle/stationary.py stationary_hist.
+//
+// Every workgroup reads the same published partial sums and adds them in the same order,
+// so all workgroups of a cluster compute bit-identical scalars and take the same branches
+// (the barrier counts stay in step).  T is column-stochastic, so sum(x) is preserved by
+// every update (sum(r) = sum(v) = sum(p) = 0).  The shadow residual rh is a fixed hash
+// of the point index (rh = r0 would need one more resident vector); rh has no mean, so
+// <rh, r> does not vanish on the zero-sum residuals.  x lives in `mass` (HBM, own columns
+// only, read-modify-written twice per step); r, p and the matvec result in registers, v in
+// LDS behind the spans and p in an HBM scratch row across the second matvec.
+#include "common.h"
+#include "internal.h"
+#include "hist_cluster.h"
+
+namespace aiy {
+
+constexpr int kHkRed = kHcRedRec;   // doubles per (parity, workgroup) partial-sum record
+
+// shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
+__device__ __forceinline__ double hk_rhat(unsigned q) {
+  unsigned h = q * 0x9E3779B1u + 0x7F4A7C15u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (double)(int)h * (1.0 / 2147483648.0);
+}
+
+// Phase timing (diagnostic builds, -DAIY_DIAG_PHASES=<block>): time since the previous
+// mark is added to slot k: 0 push, 1 publish, 2 matvec barrier, 3 gather + mix,
+// 4 reductions (partials, publish, barrier, read), 5 vector updates
+#ifdef AIY_DIAG_PHASES
+#define HK_PH(k)                                                        \
+  do {                                                                  \
+    if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES) {                    \
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();   \
+      if ((k) >= 0) ph[(k)] += tn - tq;                                 \
+      tq = tn;                                                          \
+    }                                                                   \
+  } while (0)
+#else
+#define HK_PH(k) \
+  do {           \
+  } while (0)
+#endif
+
+template <int SMAX, int KC, int TH>
+__global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
+  constexpr bool kVlds = SMAX <= 8;
+#ifdef AIY_DIAG_PHASES
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tq = 0;
+#endif
+  extern __shared__ double Tacc[];
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ int s_cinfo[KC * SMAX * TH];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
+  const int G = r.G, S = r.S, n_a = r.n_a, cap = r.cap;
+  const int lc = blockIdx.x / G;
+  const int w = blockIdx.x - lc * G;
+  const int cal = r.cal0 + lc;
+  const int j0 = w * r.nj;
+  const int j1 = min(j0 + r.nj, n_a);
+  unsigned* ctr = r.ctr + (size_t)lc * kHcCtrStride;
+  double* red = r.dist + (size_t)lc * 2 * G * kHkRed;
+  const size_t row0 = (size_t)cal * S;
+  const int* LO = r.lo + row0 * n_a;
+  const double* WL = r.wlo + row0 * n_a;
+  double* X = r.mass + row0 * n_a;   // x: the iterate, own columns read-modify-written
+  double* slab_cl = r.slab + (size_t)lc * G * 2 * cap;
+  const double* __restrict__ Pc = r.P + (size_t)cal * S * S;
+  int* span_cl = r.span + (size_t)lc * G * SMAX * 4;
+
+  // ---- setup (as hist_cluster_kernel): P, own spans, covering candidates ----
+  for (int q = tid; q < SMAX * SMAX; q += TH) {
+    const int s = q / SMAX, sp = q - s * SMAX;
+    s_P[q] = (s < S && sp < S) ? Pc[s * S + sp] : 0.0;
+  }
+  if (tid == 0) {
+    int tot = 0;
+    unsigned bad = 0;
+    for (int s = 0; s < S; ++s) {
+      const int f = LO[(size_t)s * n_a + j0];
+      const int l = LO[(size_t)s * n_a + j1 - 1] - f + 2;
+      if (l < 2 || f < 0 || f + l > n_a) bad = 2u;
+      const int ll = l > 0 ? l : 0;
+      s_base[s] = tot - f;
+      s_pub[2 * s][0] = tot;
+      s_pub[2 * s][1] = tot + max(0, min(ll, j0 - f));
+      s_pub[2 * s + 1][0] = tot + min(ll, max(0, j1 - f));
+      s_pub[2 * s + 1][1] = tot + ll;
+      int* sp = &span_cl[((size_t)w * SMAX + s) * 4];
+      __hip_atomic_store(&sp[0], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[1], ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[2], tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot += ll;
+    }
+    s_tot = tot;
+    if (tot > cap) bad = 2u;
+    if (bad) __hip_atomic_store(r.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  unsigned nb = 0;   // cluster barriers passed
+  auto barrier = [&]() -> bool {
+    ++nb;
+    return hc_barrier(r, ctr, (unsigned)G * nb, &s_flag);
+  };
+  if (!barrier()) return;
+  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  __syncthreads();
+  if (s_stop) return;
+  if (tid < S) {
+    const int s = tid;
+    int n = 0, bad = 0;
+    for (int w2 = 0; w2 < G; ++w2) {
+      const int* sp = &span_cl[((size_t)w2 * SMAX + s) * 4];
+      const int f = __hip_atomic_load(&sp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int l = __hip_atomic_load(&sp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (f < j1 && f + l > j0) {
+        const int base = __hip_atomic_load(&sp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, base};
+        else bad = 1;
+        ++n;
+      }
+    }
+    s_ncand[s] = n < kHcCand ? n : kHcCand;
+    if (bad) {
+      __hip_atomic_store(r.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  const int total = s_tot;
+  for (int q = tid; q < total; q += TH) Tacc[q] = 0.0;
+  if (!barrier()) return;
+  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  __syncthreads();
+  if (s_stop) return;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int d = j0 + tid + k * TH;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      int cf = 0, cn = 0;
+      if (s < S && d < j1) {
+        const int nc = s_ncand[s];
+        for (int c = 0; c < nc; ++c) {
+          const HcCand cd = s_cand[s][c];
+          if (d >= cd.first && d < cd.first + cd.len) {
+            if (cn == 0) cf = c;
+            ++cn;
+          }
+        }
+      }
+      s_cinfo[(k * SMAX + s) * TH + tid] = cf | (cn << 8);
+    }
+  }
+  constexpr bool kLoReg = SMAX <= 8 && KC == 1;   // with two columns per thread the registers hold the Krylov vectors
+  int dreg[KC][kLoReg ? SMAX : 1];
+  double wreg[KC][kLoReg ? SMAX : 1];
+  if constexpr (kLoReg) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = j0 + tid + k * TH;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const bool ok = s < S && j < j1;
+        dreg[k][s] = ok ? LO[(size_t)s * n_a + j] : -1;
+        wreg[k][s] = ok ? WL[(size_t)s * n_a + j] : 0.0;
+      }
+    }
+  }
+  const int v_base = lane < S ? s_base[lane] : 0;
+  const int v_plo = lane < 2 * S ? s_pub[lane][0] : 0;
+  const int v_phi = lane < 2 * S ? s_pub[lane][1] : 0;
+  // the column index is re-materialised per phase through an empty asm: otherwise the
+  // compiler hoists every point's address, hash and predicate out of the loop and keeps
+  // them live across the gathers (hundreds of VGPRs of spills)
+  const int jbase = j0 + tid;
+  auto col = [&]() {
+    int c = jbase;
+    asm volatile("" : "+v"(c));
+    return c;
+  };
+
+  // ---- the matvec pieces ----
+  // push q's own sources into the LDS spans (np.add.at(T[s], lo, wlo q) and lo + 1)
+  auto push = [&](const double (&q)[KC][SMAX]) {
+    // lottery rows in groups whose loads (L2) are all in flight before the first atomic
+    constexpr int PR = SMAX <= 8 ? SMAX : 4;
+    const int jc = col();   // lottery addresses formed here, not hoisted (they spilled)
+#pragma unroll
+    for (int s0 = 0; s0 < SMAX; s0 += PR) {
+      if (s0 < S) {
+        int dd[KC][PR];
+        double ww[KC][PR];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int j = jc + k * TH;
+#pragma unroll
+          for (int u = 0; u < PR; ++u) {
+            const int s = s0 + u;
+            if constexpr (kLoReg) {
+              dd[k][u] = s < SMAX ? dreg[k][s < SMAX ? s : 0] : -1;
+              ww[k][u] = s < SMAX ? wreg[k][s < SMAX ? s : 0] : 0.0;
+            } else {
+              // unconditional loads at a clamped index (no exec-masked branch per load)
+              const bool ok = s < S && j < j1;
+              const int q = min(s, S - 1) * n_a + min(j, n_a - 1);
+              const int dv = LO[q];
+              const double wv = WL[q];
+              dd[k][u] = ok ? dv : -1;
+              ww[k][u] = ok ? wv : 0.0;
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const bool act = j0 + tid + k * TH < j1;
+#pragma unroll
+          for (int u = 0; u < PR; ++u) {
+            const int s = s0 + u;
+            if (s < S) {   // wave-uniform
+              const int d = dd[k][u];
+              const double vlo = ww[k][u] * q[k][s];          // np.add.at(T[s], lo, wlo q)
+              const double vhi = (1.0 - ww[k][u]) * q[k][s];  // np.add.at(T[s], lo + 1, (1 - wlo) q)
+              const int ilo = __builtin_amdgcn_readlane(v_base, s) + d, ihi = ilo + 1;
+              const int d0 = __builtin_amdgcn_readfirstlane(d);
+              if (__all(act && d == d0)) {   // the whole wave on one destination (borrowing constraint)
+                const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
+                if (lane == kWave - 1) {
+                  atomicAdd(&Tacc[ilo], tl);
+                  if (th != 0.0) atomicAdd(&Tacc[ihi], th);
+                }
+              } else if (act) {
+                if (vlo != 0.0) atomicAdd(&Tacc[ilo], vlo);
+                if (vhi != 0.0) atomicAdd(&Tacc[ihi], vhi);
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+  // publish the foreign parts of the spans write-through to slab `par`, re-zero them
+  auto publish = [&](int par) {
+    double* slab = slab_cl + ((size_t)w * 2 + par) * cap;
+    for (int rr = 0; rr < 2 * S; ++rr) {
+      const int lo = __builtin_amdgcn_readlane(v_plo, rr), hi = __builtin_amdgcn_readlane(v_phi, rr);
+      for (int q = lo + tid; q < hi; q += TH) {
+        store_f64_agent(&slab[q], Tacc[q]);
+        Tacc[q] = 0.0;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // gather the own destinations (ascending covering workgroup) and mix: Tq[k][s'] =
+  // sum_s P[s, s'] T_s[d]
+  auto gather_mix = [&](int par, double (&out)[KC][SMAX]) {
+    constexpr int GR = 4;
+    double T[KC][SMAX];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) T[k][s] = 0.0;
+    bool more = false;
+#pragma unroll
+    for (int s0 = 0; s0 < SMAX; s0 += GR) {
+      if (s0 < S) {
+        double v0[KC][GR], v1[KC][GR];
+        int oq[KC][GR];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int d = j0 + tid + k * TH;
+#pragma unroll
+          for (int q = 0; q < GR; ++q) {
+            const int s = s0 + q;
+            v0[k][q] = 0.0;
+            v1[k][q] = 0.0;
+            oq[k][q] = -1;
+            if (s < S) {
+              const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+              if (cn >= 1) {
+                const HcCand c = s_cand[s][cf];
+                if (c.w != w) v0[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
+              }
+              if (cn >= 2) {
+                const HcCand c = s_cand[s][cf + 1];
+                if (c.w != w) v1[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
+              }
+              more = more || cn > 2;
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int q = 0; q < GR; ++q)
+            if (oq[k][q] >= 0) {
+              T[k][s0 + q] = Tacc[oq[k][q]];
+              Tacc[oq[k][q]] = 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int q = 0; q < GR; ++q) T[k][s0 + q] = (v0[k][q] + v1[k][q]) + T[k][s0 + q];
+      }
+    }
+    if (__any(more)) {   // columns covered by more than two spans (the borrowing constraint)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const int d = j0 + tid + k * TH;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          if (s < S) {
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+            for (int c0 = 2; c0 < cn; c0 += 4) {
+              double x[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u;
+                x[u] = 0.0;
+                if (c < cn) x[u] = hc_take(s_cand[s][cf + c], w, d, par, cap, slab_cl, Tacc);
+              }
+              T[k][s] += ((x[0] + x[1]) + x[2]) + x[3];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int sp = 0; sp < SMAX; ++sp) {
+      double pc[SMAX];
+      asm volatile("" ::: "memory");   // one column of P at a time (else all of P is hoisted)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) pc[s] = s_P[s * SMAX + sp];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) acc += pc[s] * T[k][s];
+        out[k][sp] = acc;
+      }
+    }
+  };
+  // one matvec: out = T q (the cluster exchange in the middle)
+  auto matvec = [&](const double (&q)[KC][SMAX], double (&out)[KC][SMAX]) -> bool {
+    HK_PH(5);
+    push(q);
+    HK_PH(0);
+    const int par = (int)((nb + 1) & 1);
+    publish(par);
+    HK_PH(1);
+    if (!barrier()) return false;
+    HK_PH(2);
+    gather_mix(par, out);
+    HK_PH(3);
+    return true;
+  };
+  // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
+  // fixed order at every level, so every workgroup gets the same s_res
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax) -> bool {
+    HK_PH(5);
+#pragma unroll
+    for (int v = 0; v < kHkRed; ++v) {
+      if (v < nv) {
+        const double x = (kmax >> v) & 1u ? wave_nan_max(vals[v]) : wave_sum_lane63(vals[v]);
+        if (lane == kWave - 1) s_part[v][wid] = x;
+      }
+    }
+    __syncthreads();
+    const int par = (int)((nb + 1) & 1);
+    if (tid < nv) {
+      const int v = tid;
+      double x = s_part[v][0];
+      for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
+      store_f64_agent(&red[((size_t)par * G + w) * kHkRed + v], x);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!barrier()) return false;
+    if (wid == 0) {   // every record load in flight before the first sum
+      double xa[kHkRed], xb[kHkRed];
+#pragma unroll
+      for (int v = 0; v < kHkRed; ++v) {
+        xa[v] = xb[v] = 0.0;
+        if (v < nv) {
+          if (lane < G) xa[v] = load_f64_agent(&red[((size_t)par * G + lane) * kHkRed + v]);
+          if (lane + kWave < G) xb[v] = load_f64_agent(&red[((size_t)par * G + lane + kWave) * kHkRed + v]);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < kHkRed; ++v) {
+        if (v < nv) {
+          const bool mx = (kmax >> v) & 1u;
+          const double y = mx ? wave_nan_max(nan_max(xa[v], xb[v])) : wave_sum_lane63(xa[v] + xb[v]);
+          if (lane == kWave - 1) s_res[v] = y;
+        }
+      }
+    }
+    __syncthreads();
+    HK_PH(4);
+    return true;
+  };
+
+  // ---- BiCGSTAB ----
+  // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
+  // p in the HBM scratch row across the second matvec, whose gather needs the registers
+  double rv[KC][SMAX], pv[KC][SMAX], tv[KC][SMAX];
+  // v: in LDS behind the spans when it fits (SMAX <= 8), else a per-workgroup HBM block of
+  // the same [KC][SMAX][TH] layout (behind the p rows of the scratch)
+  double* Vl = kVlds ? Tacc + cap
+                     : r.dbuf + (size_t)r.n_cal * S * n_a + (size_t)blockIdx.x * (KC * SMAX * TH);
+  double* Pg = r.dbuf + row0 * n_a;
+  auto vidx = [&](int k, int s) { return (k * SMAX + s) * TH + tid; };
+  double part[kHkRed];
+  const double tol = r.tol;
+  int mv = 0;                 // matvecs
+  bool restart = true, first = true;
+  double rho = 0.0;
+  auto own = [&](int jc, int k, int s) { return s < S && jc + k * TH < j1; };
+  auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH)); };
+  auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
+  while (true) {
+    if (restart) {
+      // true residual of x: pv = x, tv = T x, rv = T x - x
+      int jc = col();
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          const double xv = X[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
+          pv[k][s] = own(jc, k, s) ? xv : 0.0;
+        }
+      if (!matvec(pv, tv)) return;
+      ++mv;
+      jc = col();
+      double rr = 0.0, rm = 0.0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          rv[k][s] = tv[k][s] - pv[k][s];
+          if (own(jc, k, s)) {
+            rr += rh_at(jc, k, s) * rv[k][s];
+            rm = nan_max(rm, fabs(rv[k][s]));
+          }
+        }
+      part[0] = rr;
+      part[1] = rm;
+      if (!reduce(part, 2, 2u)) return;
+      rho = s_res[0];
+      if (s_res[1] < tol || mv >= r.max_iter) {   // converged (np.max(...) < tol: NaN never is)
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int s = 0; s < SMAX; ++s)
+            if (own(jc, k, s)) X[gidx(jc, k, s)] = tv[k][s];
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) pv[k][s] = rv[k][s];
+      restart = false;
+      first = true;
+    }
+    // v = p - T p (to LDS); alpha = rho / <rh, v>; the previous step's max|r| rides along.
+    // r waits in v's slot during this matvec (only p and the result stay in registers)
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) Vl[vidx(k, s)] = rv[k][s];
+    if (!matvec(pv, tv)) return;
+    ++mv;
+    int jc = col();
+    double rvv = 0.0, rm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const double v = pv[k][s] - tv[k][s];
+        rv[k][s] = Vl[vidx(k, s)];
+        Vl[vidx(k, s)] = v;
+        if (own(jc, k, s)) {
+          rvv += rh_at(jc, k, s) * v;
+          rm = nan_max(rm, fabs(rv[k][s]));
+        }
+      }
+    part[0] = rvv;
+    part[1] = rm;
+    if (!reduce(part, 2, 2u)) return;
+    if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
+      restart = true;
+      continue;
+    }
+    first = false;
+    const double alpha = rho / s_res[0];
+    if (!(fabs(alpha) < 1e300)) {   // breakdown (<rh, v> = 0) or NaN: restart from the true residual
+      restart = true;
+      continue;
+    }
+    // x += alpha p; p -> HBM scratch; s = r - alpha v (in rv); t = s - T s (in tv)
+    jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        {
+          const int g = min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1);
+          const double xv = X[g];
+          if (own(jc, k, s)) {
+            X[g] = xv + alpha * pv[k][s];
+            Pg[g] = pv[k][s];
+          }
+        }
+        rv[k][s] -= alpha * Vl[vidx(k, s)];
+      }
+    if (!matvec(rv, tv)) return;
+    ++mv;
+    jc = col();
+    double ts = 0.0, tt = 0.0, rs = 0.0, rt = 0.0, sm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        tv[k][s] = rv[k][s] - tv[k][s];
+        if (own(jc, k, s)) {
+          const double h = rh_at(jc, k, s);
+          ts += tv[k][s] * rv[k][s];
+          tt += tv[k][s] * tv[k][s];
+          rs += h * rv[k][s];
+          rt += h * tv[k][s];
+          sm = nan_max(sm, fabs(rv[k][s]));
+        }
+      }
+    part[0] = ts;
+    part[1] = tt;
+    part[2] = rs;
+    part[3] = rt;
+    part[4] = sm;
+    if (!reduce(part, 5, 16u)) return;
+    double omega = (s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1];
+    if (!(fabs(omega) < 1e300)) omega = 0.0;
+    if (omega == 0.0) {   // s already below tol (x + alpha p is the answer), or <t, t> = 0: verify
+      restart = true;
+      continue;
+    }
+    const double rho2 = s_res[2] - omega * s_res[3];
+    const double beta = (rho2 / rho) * (alpha / omega);
+    rho = rho2;
+    // x += omega s; r = s - omega t; p = r + beta (p - omega v)
+    jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const int g = min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1);
+        const double xv = X[g], pg = Pg[g];
+        const bool ow = own(jc, k, s);
+        if (ow) X[g] = xv + omega * rv[k][s];
+        const double pold = ow ? pg : 0.0;
+        rv[k][s] = rv[k][s] - omega * tv[k][s];
+        pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
+      }
+    if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
+  }
+  if (w == 0 && tid == 0) r.iters_out[cal] = mv;
+#ifdef AIY_DIAG_PHASES
+  if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES && mv > 0)
+    printf("[bicg phases] block %d G=%d nj=%d matvecs=%d us/matvec: push %.2f publish %.2f barrier %.2f gather+mix "
+           "%.2f reduce %.2f vector %.2f\n",
+           (int)blockIdx.x, G, r.nj, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv, ph[3] * 0.01 / mv,
+           ph[4] * 0.01 / mv, ph[5] * 0.01 / mv);
+#endif
+}
+
+template <int SMAX, int KC, int TH>
+static const void* hk_fn() {
+  return reinterpret_cast<const void*>(hist_bicg_kernel<SMAX, KC, TH>);
+}
+
+// kernel for the plan's (S, padded S, columns per thread) and its state count SMAX
+// (*smax_k); nullptr when there is no instantiation
+const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k) {
+  *smax_k = smax;
+  if (S == 7 && kc == 2) return *smax_k = 7, hk_fn<7, 2, 512>();
+  if (smax == 8) return kc == 1 ? hk_fn<8, 1, 512>() : hk_fn<8, 2, 512>();
+  if (kc != 1) return nullptr;
+  if (smax == 16) return hk_fn<16, 1, 512>();
+  if (S == 25) return *smax_k = 25, hk_fn<25, 1, 512>();
+  return hk_fn<32, 1, 512>();
+}
+
+}  // namespace aiy

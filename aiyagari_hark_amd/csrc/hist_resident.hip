@@ -30,67 +30,12 @@
 // runs the push/mix pair instead.
 #include "common.h"
 #include "internal.h"
+#include "hist_cluster.h"
 
 #include <algorithm>
 #include <type_traits>
 
 namespace aiy {
-
-constexpr int kHcMaxG = 128;                       // workgroups per calibration cluster
-constexpr int kHcCand = 32;                        // covering workgroups per (row, workgroup)
-constexpr int kHcRows = 8;                         // rows whose push loads are in flight together
-// rows whose gather loads are in flight together: all (S <= 8) for one column per thread
-template <int SMAX, int KC, int TH>
-struct HcGather {
-  static constexpr int kRows = SMAX == 8 ? 8 : 4;
-};
-constexpr size_t kHcLdsTotal = 160 * 1024;         // per CU
-constexpr unsigned long long kHcTimeoutTicks = 200000000ull;   // 2 s of the 100 MHz clock
-constexpr int kHcCtrStride = 32;                   // uints between cluster counters (128 B)
-
-struct HcRun {
-  int n_cal, cal0, S, n_a, G, nj, cap;   // cap: doubles of the span buffer / one slab
-  const int* lo;          // [n_cal][S][n_a]
-  const double* wlo;      // [n_cal][S][n_a]
-  const double* P;        // [n_cal][S][S]
-  double* mass;           // [n_cal][S][n_a] in: start, out: final
-  double* slab;           // [launch cals][G][2][cap]
-  int* span;              // [launch cals][G][SMAX][4] (first, len, left base, right base)
-  unsigned* ctr;          // [launch cals][kHcCtrStride]
-  double* dist;           // [launch cals][2][G][4]: sup-norm change, Aitken dot products, valid
-  double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0)
-  int accel;              // Aitken extrapolation period E (0: plain iteration = the oracle's)
-  int* iters_out;         // [n_cal]
-  unsigned* err;          // 0 ok, 1 timeout, 2 span overflow / not monotone, 3 candidate overflow
-  double tol;
-  int max_iter;
-};
-
-struct HcCand {
-  int w, first, len, base;   // destination d of the covering span sits at slab/LDS index base + d
-};
-
-// Cluster barrier: lane 0 adds one to the cluster counter (after the caller's drained sc1
-// stores) and waits until it reaches `target`.  False on timeout (error word set).
-__device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsigned target, int* s_flag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int ok = 1;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    *s_flag = ok;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
 
 #ifdef AIY_DIAG_PHASES
 #define HC_PH(k)                                                        \
@@ -106,41 +51,6 @@ __device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsign
   do {           \
   } while (0)
 #endif
-
-// One covering span's value at destination d: the own span from LDS (read once by the
-// column's owner, then re-zeroed for the next push), a foreign one from its published slab.
-__device__ __forceinline__ double hc_take(const HcCand& c, int w, int d, int par, int cap, const double* slab_cl,
-                                          double* Tacc) {
-  const int q = c.base + d;
-  // two destinations (added at the use): one shared register would make the LDS read
-  // wait for every earlier slab load in flight (write-after-write on the register)
-  double vg = 0.0, vl = 0.0;
-  if (c.w == w) {
-    vl = Tacc[q];
-    Tacc[q] = 0.0;
-  } else {
-    vg = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + q]);
-  }
-  return vg + vl;
-}
-
-// Sum over the 64 lanes (DPP: row shifts, then row broadcasts), valid in lane 63.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ double dpp_add_src(double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, ROWS, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROWS, 0xF, false);
-  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-__device__ __forceinline__ double wave_sum_lane63(double v) {
-  v += dpp_add_src<0x111, 0xF>(v);   // row_shr:1
-  v += dpp_add_src<0x112, 0xF>(v);   // row_shr:2
-  v += dpp_add_src<0x114, 0xF>(v);   // row_shr:4
-  v += dpp_add_src<0x118, 0xF>(v);   // row_shr:8   (lane 15 of every row: the row's sum)
-  v += dpp_add_src<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
-  v += dpp_add_src<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
-  return v;
-}
 
 // Cluster barrier of iteration `it` that also counts the workgroups whose last change was
 // not below tol: lane 0 adds (1 | flag << 32) to the 64-bit word of the iteration's parity
@@ -637,6 +547,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 // thread (two only with S <= 8, where the lottery and the mass stay in registers).
 struct HcPlan {
   int G = 0, nj = 0, th = 0, kc = 0, smax = 0, cals_per_launch = 0, cap = 0;
+  size_t vblock = 0;
   size_t lds = 0;
   const void* fn = nullptr;
 };
@@ -652,7 +563,7 @@ static const void* hc_pick(int smax, int kc) {
   return hc_fn<32, 1, 512>();
 }
 
-static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
+static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bool krylov = false) {
   if (S > 32 || S < 1 || n_a < 2) return false;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
@@ -669,19 +580,25 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p) {
   p.kc = p.nj <= p.th ? 1 : 2;
   if (p.kc > kc_max) return false;
   p.cals_per_launch = std::max(1, cus / p.G);
-  p.fn = hc_pick(p.smax, p.kc);
+  int smax_k = p.smax;
+  p.fn = krylov ? hist_bicg_pick(S, p.smax, p.kc, &smax_k) : hc_pick(p.smax, p.kc);
+  if (!p.fn) return false;
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
   const size_t stat = fa.sharedSizeBytes;
   if (stat + 4096 >= kHcLdsTotal) return false;
   p.lds = (kHcLdsTotal - stat - 1024) / 256 * 256;
-  p.cap = (int)(p.lds / sizeof(double));
+  // BiCGSTAB: one resident vector (v, [KC][SMAX][TH] doubles) behind the span buffer
+  const size_t vbytes = krylov && smax_k <= 8 ? (size_t)p.kc * smax_k * p.th * sizeof(double) : 0;
+  p.vblock = krylov && smax_k > 8 ? (size_t)p.kc * smax_k * p.th : 0;   // v in HBM, doubles per workgroup
+  if (p.lds <= vbytes + 4096) return false;
+  p.cap = (int)((p.lds - vbytes) / sizeof(double));
   return true;
 }
 
 static int32_t hc_scratch(aiy_handle* h, int cals, int G, int cap) {
   const size_t need = (size_t)cals * G * 2 * cap * sizeof(double) + (size_t)cals * G * 32 * 4 * sizeof(int) +
-                      (size_t)cals * kHcCtrStride * sizeof(unsigned) + (size_t)cals * 2 * G * 4 * sizeof(double) +
+                      (size_t)cals * kHcCtrStride * sizeof(unsigned) + (size_t)cals * 2 * G * kHcRedRec * sizeof(double) +
                       256;
   if (need > h->hc_cap) {
     if (h->d_hc) (void)hipFree(h->d_hc);
@@ -700,7 +617,8 @@ static int32_t hc_scratch(aiy_handle* h, int cals, int G, int cap) {
 int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int* lo, const double* wlo,
                             const double* P, double tol, int max_iter, double* mass, int* d_iters, hipStream_t st) {
   HcPlan p;
-  if (!hc_make_plan(h, n_cal, S, n_a, p)) return AIY_ERR_UNSUPPORTED;
+  const bool krylov = h->hist_krylov != 0;
+  if (!hc_make_plan(h, n_cal, S, n_a, p, krylov)) return AIY_ERR_UNSUPPORTED;
   AIY_HIP(h, hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
   int per_cu = 0;
   AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds));
@@ -720,12 +638,12 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   const size_t ctr_bytes = (size_t)per_launch * kHcCtrStride * sizeof(unsigned);
   off += ctr_bytes;
   r.dist = reinterpret_cast<double*>(base + off);
-  off += (size_t)per_launch * 2 * p.G * 4 * sizeof(double);
-  r.accel = h->hist_accel;
+  off += (size_t)per_launch * 2 * p.G * kHcRedRec * sizeof(double);
+  r.accel = krylov ? 0 : h->hist_accel;
   r.dbuf = nullptr;
-  if (r.accel > 0) {
-    if (r.accel < 4) r.accel = 4;
-    const size_t db = (size_t)n_cal * S * n_a * sizeof(double);
+  if (r.accel > 0 || krylov) {   // Aitken: stored differences; BiCGSTAB: the p scratch rows
+    if (r.accel > 0 && r.accel < 4) r.accel = 4;
+    const size_t db = ((size_t)n_cal * S * n_a + (size_t)per_launch * p.G * p.vblock) * sizeof(double);
     if (db > h->hc_dcap) {
       if (h->d_hcd) (void)hipFree(h->d_hcd);
       h->d_hcd = nullptr;

@@ -41,6 +41,7 @@ struct aiy_handle {
   bool hist_resident = true;         // AIY_OPT_HIST_RESIDENT (hist_resident.hip)
   int hist_cluster_cap = 0;          // AIY_OPT_HIST_CLUSTER: max workgroups per calibration (0: 32)
   int hist_accel = 0;                // AIY_OPT_HIST_ACCEL: Aitken period of the resident histogram (0: off)
+  int hist_krylov = 0;               // AIY_OPT_HIST_KRYLOV: resident histogram solves by BiCGSTAB
   void* d_hcd = nullptr;             // resident histogram: stored differences (Aitken)
   size_t hc_dcap = 0;
   void* d_hc = nullptr;              // resident histogram: slabs, spans, counters, distances

@@ -455,6 +455,7 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       if (value < 0 || value > (1 << 20)) return fail(h, AIY_ERR_ARG, "AIY_OPT_HIST_ACCEL must be >= 0");
       h->hist_accel = (int)value;
       return AIY_OK;
+    case AIY_OPT_HIST_KRYLOV: h->hist_krylov = value != 0; return AIY_OK;
     case AIY_OPT_HIST_CLUSTER:
       if (value < 0 || value > 128) return fail(h, AIY_ERR_ARG, "AIY_OPT_HIST_CLUSTER must be in [0, 128]");
       h->hist_cluster_cap = (int)value;

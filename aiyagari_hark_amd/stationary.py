@@ -123,7 +123,10 @@ class StationaryBatch:
         lets the device-resident distribution iteration extrapolate along its slowest mode
         every E iterations (Aitken, AIY_OPT_HIST_ACCEL): the same fixed point to the
         iteration's own accuracy (~1e-7 relative in K), 1.5-3x fewer
-        iterations; 0 is the oracle's plain iteration."""
+        iterations; accel < 0 solves (I - T) mass = 0 by BiCGSTAB (AIY_OPT_HIST_KRYLOV,
+        hist_krylov.hip): a mass T x with max|T x - x| < hist_tol, the plain iteration's
+        stopping rule, in 10-20x fewer matvecs (counts are matvecs); 0 is the oracle's
+        plain iteration."""
         n_cal, S = len(self.cals), self.S
         r = np.asarray(r, dtype=np.float64)
         w, _ = firm_prices(r, self.alpha, self.delta)
@@ -146,13 +149,15 @@ class StationaryBatch:
             self.mass.fill_(1.0 / (S * self.n_a))
         K = (ctypes.c_double * n_cal)()
         iters = (ctypes.c_int32 * n_cal)()
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_ACCEL, int(accel)), "aiy_set_option")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_ACCEL, max(int(accel), 0)), "aiy_set_option")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_KRYLOV, int(accel < 0)), "aiy_set_option")
         try:
             h.check(h.lib.aiy_hist_solve(h.h, n_cal, S, self.n_a, _lib.ptr(self.lo), _lib.ptr(self.wlo),
                                          _lib.ptr(self.d_P), _lib.ptr(self.d_a), float(hist_tol), int(max_hist), 64,
                                          _lib.ptr(self.mass), _lib.ptr(self.work), K, iters, sp), "aiy_hist_solve")
         finally:
             h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_ACCEL, 0), "aiy_set_option")
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_KRYLOV, 0), "aiy_set_option")
         self.last_tables = (m, c)
         self._mass_valid = True
         return np.array(K[:]), np.array(cycles), np.array(iters[:])
@@ -275,9 +280,9 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     warm_hist: each step's distribution iteration starts from the previous step's
     stationary mass (the oracle, oracle/stationary.py, starts from uniform; both converge
     to the same distribution to hist_tol).  warm_egm (default: on for "brent"): each
-    step's household solve starts from the previous step's policy.  accel (default: 32
-    for "brent", 0 for "bisect"): Aitken period of the distribution iteration
-    (StationaryBatch.capital_supply).
+    step's household solve starts from the previous step's policy.  accel (default: -1 =
+    BiCGSTAB for "brent", 0 = the plain iteration for "bisect"; E > 0: Aitken period) --
+    the distribution solver (StationaryBatch.capital_supply).
     engine: "native" -- one aiy_ge_stationary call (C++ search loop); "python" -- the same
     search driven from Python step by step (per-step logs; identical iterates)."""
     cals = table2_calibrations() if cals is None else list(cals)
@@ -290,7 +295,7 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     if warm_egm is None:
         warm_egm = method == "brent"
     if accel is None:
-        accel = 32 if method == "brent" else 0
+        accel = -1 if method == "brent" else 0
     steps = 0
     cyc_log, it_log = [], []
     Ks = np.zeros(n)

@@ -337,6 +337,10 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     contraction ratio agree (Aitken; same fixed point, fewer
                                     iterations, counts differ from the plain iteration); 0 (default):
                                     the plain iteration of oracle/stationary.py */
+#define AIY_OPT_HIST_KRYLOV 9     /* value != 0: the resident histogram solves (I - T) mass = 0 by
+                                    BiCGSTAB from the given mass (hist_krylov.hip; stops at a mass
+                                    T x with max|T x - x| < tol, the plain iteration's rule; counts
+                                    are matvecs); takes precedence over AIY_OPT_HIST_ACCEL */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
@@ -391,7 +395,7 @@ typedef struct {
   int32_t max_steps, max_egm_cycles, max_hist_iter;
   int32_t warm_hist;     /* != 0: each step's distribution starts from the previous step's     */
   int32_t warm_egm;      /* != 0: each step's household solve starts from the previous policy */
-  int32_t accel;         /* Aitken period of the distribution iteration (0: plain)            */
+  int32_t accel;         /* Aitken period of the distribution iteration (0: plain; < 0: BiCGSTAB) */
   const double* r_lo;    /* HOST [n_cal] or NULL: -delta / 2                                   */
   const double* r_hi;    /* HOST [n_cal] or NULL: 1 / beta - 1 - 1e-9                          */
 } aiy_ge_options;

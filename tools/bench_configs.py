@@ -60,7 +60,7 @@ def stress(n_a, device):
             for c in (1.0, 3.0, 5.0)]
     torch.cuda.synchronize()
     t = time.perf_counter()
-    res = solve_table2(cals, n_a=n_a, device=device)
+    res = solve_table2(cals, n_a=n_a, device=device, method="brent")
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     pts = int(np.sum([np.sum(i) for i in res.hist_iters])) * 25 * n_a

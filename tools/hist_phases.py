@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """One K_s(r) evaluation of the 24 Table II calibrations (N_a = 10 000) through the
 library named by AIYAGARI_LIB (e.g. the AIY_DIAG_PHASES variant, which prints per-phase
-times of the resident histogram); prints wall time and iteration counts."""
+times of the resident histogram); prints wall time and iteration counts.
+Arguments: [n_cal] [cluster cap] [accel: Aitken period, < 0 BiCGSTAB]."""
 import json
 import os
 import sys
@@ -19,6 +20,7 @@ def main():
     from aiyagari_hark_amd.stationary import StationaryBatch, table2_calibrations
     n_cal = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     cluster = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    accel = int(sys.argv[3]) if len(sys.argv) > 3 else 32   # < 0: BiCGSTAB (hist_krylov.hip)
     dev = torch.device("cuda:0")
     h = _lib.handle(0)
     h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, cluster), "opt")
@@ -28,7 +30,7 @@ def main():
     for rep in range(2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        K, cyc, it = b.capital_supply(r)
+        K, cyc, it = b.capital_supply(r, accel=accel)
         torch.cuda.synchronize()
         print(json.dumps(dict(n_cal=n_cal, cluster=cluster, rep=rep, seconds=time.perf_counter() - t0,
                               hist_iters_max=int(np.max(it)), egm_cycles_max=int(np.max(cyc)))), flush=True)
