@@ -18,7 +18,7 @@ struct HcGather {
 constexpr size_t kHcLdsTotal = 160 * 1024;         // per CU
 constexpr unsigned long long kHcTimeoutTicks = 200000000ull;   // 2 s of the 100 MHz clock
 constexpr int kHcCtrStride = 32;
-constexpr int kHcRedRec = 8;                      // doubles per (parity, workgroup) record of `dist`                   // uints between cluster counters (128 B)
+constexpr int kHcRedRec = 16;                     // 8-byte words per (parity, workgroup) record of `dist`                   // uints between cluster counters (128 B)
 
 struct HcRun {
   int n_cal, cal0, S, n_a, G, nj, cap;   // cap: doubles of the span buffer / one slab

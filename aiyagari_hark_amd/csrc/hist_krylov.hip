@@ -38,7 +38,8 @@
 
 namespace aiy {
 
-constexpr int kHkRed = kHcRedRec;   // doubles per (parity, workgroup) partial-sum record
+constexpr int kHkRed = 8;   // partial sums per reduction (at most)
+static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
 __device__ __forceinline__ double hk_rhat(unsigned q) {
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   const int j0 = w * r.nj;
   const int j1 = min(j0 + r.nj, n_a);
   unsigned* ctr = r.ctr + (size_t)lc * kHcCtrStride;
-  double* red = r.dist + (size_t)lc * 2 * G * kHkRed;
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(r.dist) + (size_t)lc * 2 * G * kHcRedRec;
   const size_t row0 = (size_t)cal * S;
   const int* LO = r.lo + row0 * n_a;
   const double* WL = r.wlo + row0 * n_a;
@@ -395,7 +396,17 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   };
   // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
   // fixed order at every level, so every workgroup gets the same s_res
-  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax) -> bool {
+  // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
+  // fixed order at every level, so every workgroup gets the same s_res.  The workgroup's
+  // values travel as tagged 8-byte granules ({epoch, 32 data bits}, two per double, sc1
+  // stores; MI355X_MICROARCH.md hand-off R2): the data is its own flag, so there is no
+  // counter barrier and no store drain -- wave 0 re-reads the cluster's granules until
+  // every tag carries this reduction's epoch.  Epochs count up from 1 within a launch (the
+  // host zeroes the granules before each launch); slots alternate by epoch parity, and a
+  // matvec barrier separates any two reductions, so a slot is rewritten only after every
+  // workgroup has read it.
+  unsigned ne = 0;   // reductions done
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, auto&& prefetch) -> bool {
     HK_PH(5);
 #pragma unroll
     for (int v = 0; v < kHkRed; ++v) {
@@ -405,25 +416,50 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
       }
     }
     __syncthreads();
-    const int par = (int)((nb + 1) & 1);
+    ++ne;
+    const unsigned long long tag = (unsigned long long)ne << 32;
+    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
     if (tid < nv) {
       const int v = tid;
       double x = s_part[v][0];
       for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
-      store_f64_agent(&red[((size_t)par * G + w) * kHkRed + v], x);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+      unsigned long long* g = slot + (size_t)w * (2 * kHkRed) + 2 * v;
+      __hip_atomic_store(g, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 1, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!barrier()) return false;
-    if (wid == 0) {   // every record load in flight before the first sum
+    prefetch();   // loads the step after the reduction needs, in flight across the sweep
+    if (wid == 0) {
       double xa[kHkRed], xb[kHkRed];
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok;
+      do {   // every granule load of a pass in flight before the tag test
+        ok = true;
 #pragma unroll
-      for (int v = 0; v < kHkRed; ++v) {
-        xa[v] = xb[v] = 0.0;
-        if (v < nv) {
-          if (lane < G) xa[v] = load_f64_agent(&red[((size_t)par * G + lane) * kHkRed + v]);
-          if (lane + kWave < G) xb[v] = load_f64_agent(&red[((size_t)par * G + lane + kWave) * kHkRed + v]);
+        for (int u = 0; u < 2; ++u) {
+          const int w2 = lane + u * kWave;
+#pragma unroll
+          for (int v = 0; v < kHkRed; ++v) {
+            double x = 0.0;
+            if (v < nv && w2 < G) {
+              const unsigned long long* g = slot + (size_t)w2 * (2 * kHkRed) + 2 * v;
+              const unsigned long long hi = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long lo = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
+              x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            }
+            if (u == 0) xa[v] = x;
+            else xb[v] = x;
+          }
         }
-      }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+          if (lane == 0) __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      } while (true);
+      if (lane == 0) s_flag = ok ? 1 : 0;
 #pragma unroll
       for (int v = 0; v < kHkRed; ++v) {
         if (v < nv) {
@@ -435,7 +471,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
     }
     __syncthreads();
     HK_PH(4);
-    return true;
+    return s_flag != 0;
   };
 
   // ---- BiCGSTAB ----
@@ -456,6 +492,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   auto own = [&](int jc, int k, int s) { return s < S && jc + k * TH < j1; };
   auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH)); };
   auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
+  HK_PH(-1);
   while (true) {
     if (restart) {
       // true residual of x: pv = x, tv = T x, rv = T x - x
@@ -483,7 +520,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
         }
       part[0] = rr;
       part[1] = rm;
-      if (!reduce(part, 2, 2u)) return;
+      if (!reduce(part, 2, 2u, [] {})) return;
       rho = s_res[0];
       if (s_res[1] < tol || mv >= r.max_iter) {   // converged (np.max(...) < tol: NaN never is)
 #pragma unroll
@@ -524,7 +561,15 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
       }
     part[0] = rvv;
     part[1] = rm;
-    if (!reduce(part, 2, 2u)) return;
+    double xq[KC][SMAX];   // x of the own points, for x += alpha p
+    if (!reduce(part, 2, 2u, [&] {
+          const int jq = col();
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
+        }))
+      return;
     if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
       restart = true;
       continue;
@@ -541,13 +586,10 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
     for (int k = 0; k < KC; ++k)
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) {
-        {
-          const int g = min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1);
-          const double xv = X[g];
-          if (own(jc, k, s)) {
-            X[g] = xv + alpha * pv[k][s];
-            Pg[g] = pv[k][s];
-          }
+        if (own(jc, k, s)) {
+          const int g = s * n_a + jc + k * TH;
+          X[g] = xq[k][s] + alpha * pv[k][s];
+          Pg[g] = pv[k][s];
         }
         rv[k][s] -= alpha * Vl[vidx(k, s)];
       }
@@ -574,7 +616,19 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
     part[2] = rs;
     part[3] = rt;
     part[4] = sm;
-    if (!reduce(part, 5, 16u)) return;
+    double pq[KC][SMAX];   // x and p of the own points, for x += omega s and the new p
+    if (!reduce(part, 5, 16u, [&] {
+          const int jq = col();
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+              const int g = min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1);
+              xq[k][s] = X[g];
+              pq[k][s] = Pg[g];
+            }
+        }))
+      return;
     double omega = (s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1];
     if (!(fabs(omega) < 1e300)) omega = 0.0;
     if (omega == 0.0) {   // s already below tol (x + alpha p is the answer), or <t, t> = 0: verify
@@ -590,11 +644,9 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
     for (int k = 0; k < KC; ++k)
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) {
-        const int g = min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1);
-        const double xv = X[g], pg = Pg[g];
         const bool ow = own(jc, k, s);
-        if (ow) X[g] = xv + omega * rv[k][s];
-        const double pold = ow ? pg : 0.0;
+        if (ow) X[s * n_a + jc + k * TH] = xq[k][s] + omega * rv[k][s];
+        const double pold = ow ? pq[k][s] : 0.0;
         rv[k][s] = rv[k][s] - omega * tv[k][s];
         pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
       }

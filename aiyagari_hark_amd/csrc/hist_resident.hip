@@ -658,6 +658,8 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
     const int nc = std::min(per_launch, n_cal - c0);
     r.cal0 = c0;
     AIY_HIP(h, hipMemsetAsync(r.ctr, 0, ctr_bytes, st));
+    if (krylov)   // reduction granules: epochs count from 1 in every launch
+      AIY_HIP(h, hipMemsetAsync(r.dist, 0, (size_t)per_launch * 2 * p.G * kHcRedRec * sizeof(double), st));
     AIY_HIP(h, hipMemsetAsync(r.err, 0, sizeof(unsigned), st));
     void* args[] = {&r};
     AIY_HIP(h, hipEventRecord(h->hc_ev[0], st));
