@@ -488,7 +488,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   const double tol = r.tol;
   int mv = 0;                 // matvecs
   bool restart = true, first = true;
-  double rho = 0.0;
+  double rho = 0.0, total0 = 0.0;
   auto own = [&](int jc, int k, int s) { return s < S && jc + k * TH < j1; };
   auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH)); };
   auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
       if (!matvec(pv, tv)) return;
       ++mv;
       jc = col();
-      double rr = 0.0, rm = 0.0;
+      double rr = 0.0, rm = 0.0, xs = 0.0;
 #pragma unroll
       for (int k = 0; k < KC; ++k)
 #pragma unroll
@@ -516,18 +516,25 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
           if (own(jc, k, s)) {
             rr += rh_at(jc, k, s) * rv[k][s];
             rm = nan_max(rm, fabs(rv[k][s]));
+            xs += pv[k][s];
           }
         }
       part[0] = rr;
       part[1] = rm;
-      if (!reduce(part, 2, 2u, [] {})) return;
+      part[2] = xs;
+      if (!reduce(part, 3, 2u, [] {})) return;
       rho = s_res[0];
+      if (mv == 1) total0 = s_res[2];   // the starting mass's total
       if (s_res[1] < tol || mv >= r.max_iter) {   // converged (np.max(...) < tol: NaN never is)
+        // T x rescaled to the start's total: the residual test cannot see the scale of x,
+        // and near a breakdown (huge alpha) rounding can move sum(x) away from it; T
+        // preserves totals, as the plain iteration does
+        const double scale = total0 / s_res[2];
 #pragma unroll
         for (int k = 0; k < KC; ++k)
 #pragma unroll
           for (int s = 0; s < SMAX; ++s)
-            if (own(jc, k, s)) X[gidx(jc, k, s)] = tv[k][s];
+            if (own(jc, k, s)) X[gidx(jc, k, s)] = mv == 1 ? tv[k][s] : tv[k][s] * scale;
         break;
       }
 #pragma unroll
