@@ -50,6 +50,13 @@ __device__ __forceinline__ double wave_max(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
   return v;
 }
+// Sum over the wave by xor butterflies (a fixed order per lane: lane 0's value is
+// reproducible run to run).
+__device__ __forceinline__ double wave_sum_fixed(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 // NaN-propagating max (np.max semantics): a NaN anywhere makes the result NaN.
 __device__ __forceinline__ double nan_max(double a, double b) {
   return (a != a || a > b) ? a : b;

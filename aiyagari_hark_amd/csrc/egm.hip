@@ -310,12 +310,47 @@ __device__ __forceinline__ void egm_prologue(const EgmDev& A, const int* __restr
   if (!TERMINAL && t < ROWS * S) st.hint[t] = hints[(size_t)W.w * ROWS * S + t];
 }
 
+// CRRA powers by a compile-time kind PK of the calibration's CRRA: 1 (log utility), 3,
+// 5 (the Table II values; integer powers and a root refined in f64) or 0 (any CRRA: the
+// device pow).  The Table II forms differ from the correctly rounded pow by a few ulp
+// (vs NumPy's pow: 1e-12 relative parity on converged tables, tests/test_gpu_parity.py);
+// the ocml f64 pow was ~40 % of a stationary 24-calibration cycle.
+//   marg_u:   c^-rho          (MargValueFuncCRRA, AS:1479-1482)
+//   inv_marg: E^(-1/rho)      (AS:1490)
+template <int PK>
+__device__ __forceinline__ double marg_u(double c, double gam) {
+  if constexpr (PK == 1) return 1.0 / c;
+  else if constexpr (PK == 3) return 1.0 / ((c * c) * c);
+  else if constexpr (PK == 5) {
+    const double c2 = c * c;
+    return 1.0 / ((c2 * c2) * c);
+  } else return pow(c, -gam);
+}
+template <int PK>
+__device__ __forceinline__ double inv_marg(double E, double gam) {
+  if constexpr (PK == 1) return 1.0 / E;
+  else if constexpr (PK == 3) return rcbrt(E);
+  else if constexpr (PK == 5) {
+    // y = E^(-1/5): f32 estimate, two Newton steps on y^-5 = E (y += y (1 - E y^5) / 5);
+    // outside the f32 range (or NaN) the f64 pow
+    if (!(E > 1e-30 && E < 1e30)) return pow(E, -0.2);
+    double y = (double)powf((float)E, -0.2f);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const double y2 = y * y;
+      const double e = 1.0 - E * ((y2 * y2) * y);
+      y = y + y * (e * 0.2);
+    }
+    return y;
+  } else return pow(E, -1.0 / gam);
+}
+
 // Phase 1: V[s'][i] = R[k,s'] c_{s'}(m'(i,k,s'), M'[k,s'])^-rho for s' = wave, wave + 4, ...
 // Rows (s', j - 1) and (s', j) of the next-period tables are visited in order; the
 // window of the next row is loaded while the current one is searched (software
-// pipeline).  LOG: CRRA == 1 at compile time (with a runtime select the compiler
+// pipeline).  PK: the CRRA power kind at compile time (with a runtime select the compiler
 // evaluated the f64 pow unconditionally).
-template <int SC, bool TERMINAL, bool LOG, int ROWS>
+template <int SC, bool TERMINAL, int PK, int ROWS>
 __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __restrict__ m_next,
                                            const double* __restrict__ c_next, const EgmWork& W, int wave,
                                            double a, double* Vs,
@@ -329,7 +364,7 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
     for (int sp = wave; sp < S; sp += kEgmWaves) {
       const double R = st.R[sp];
       const double c = (R * a + st.Wl[sp]) * 1.0;   // IdentityFunction (AS:898) of mNextArray (AS:1024)
-      const double vP = LOG ? 1.0 / c : pow(c, -gam);     // MargValueFuncCRRA
+      const double vP = marg_u<PK>(c, gam);                // MargValueFuncCRRA
       Vs[sp * kTile + lane] = R * vP;                    // RnextArray * vPnext
     }
     return;
@@ -362,7 +397,7 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
         const double al = st.al[sp];
         c = (1 - al) * f0 + al * f1;
       }
-      const double vP = LOG ? 1.0 / c : pow(c, -gam);
+      const double vP = marg_u<PK>(c, gam);
       Vs[sp * kTile + lane] = st.R[sp] * vP;
     };
     // rows whose window did not hold every lane's bracket: redone below, from global
@@ -442,7 +477,7 @@ __device__ __forceinline__ void egm_phase1(const EgmDev& A, const double* __rest
 // LDS, P[s,:] wave-uniform from LDS (broadcast reads) -- then c = E^(-1/rho),
 // m = a + c (AS:1490-1499), written row-contiguous in i.  Returns the block-local part
 // of the HARK distance; the previous table's values it compares with are loaded first.
-template <int SMAX, int SC, bool LOG>
+template <int SMAX, int SC, int PK>
 __device__ __forceinline__ double egm_phase2(const EgmDev& A, const double* __restrict__ m_next,
                                              const double* __restrict__ c_next, double* __restrict__ m_out,
                                              double* __restrict__ c_out, const EgmWork& W, int wave, int i,
@@ -478,7 +513,7 @@ __device__ __forceinline__ double egm_phase2(const EgmDev& A, const double* __re
     else
       sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vs[t * kTile + lane] * uniform_f64(Ps[t]); });
     const double E = beta * sum;                              // EndOfPrdvP (AS:1485)
-    const double c = LOG ? 1.0 / E : pow(E, -1.0 / gam);      // AS:1490
+    const double c = inv_marg<PK>(E, gam);                    // AS:1490
     const double m = a + c;                                   // AS:1499
     const size_t row = tab_cal + ((size_t)s * n_M + k) * n1;
     m_out[row + i + 1] = m;
@@ -567,17 +602,23 @@ __global__ __launch_bounds__(kEgmBlock, (SC > 0 || SMAX <= 16) ? AIY_EGM_WAVES_P
   const bool track = (dist_slots != nullptr) && cycle >= 2;
   __syncthreads();
   AIY_EGM_STAMP(W, 2);
-  const bool log_util = s_par[0] == 1.0;   // block-uniform: one of two straight-line bodies
+  // block-uniform power kind: one straight-line body per kind
+  const double crra = s_par[0];
+  const int pk = crra == 1.0 ? 1 : (crra == 3.0 ? 3 : (crra == 5.0 ? 5 : 0));
   double* X = s_win[wave];   // slices: X | Y | XB | YB
   double* Y = X + kWin;
 #if AIY_EGM_DIAG == 1
   for (int sp = wave; sp < A.S; sp += kEgmWaves) Vs[sp * kTile + (threadIdx.x & (kWave - 1))] = a + sp;
   if (false)
 #endif
-  if (log_util)
-    egm_phase1<SC, TERMINAL, true, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
+  if (pk == 1)
+    egm_phase1<SC, TERMINAL, 1, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
+  else if (pk == 3)
+    egm_phase1<SC, TERMINAL, 3, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
+  else if (pk == 5)
+    egm_phase1<SC, TERMINAL, 5, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
   else
-    egm_phase1<SC, TERMINAL, false, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
+    egm_phase1<SC, TERMINAL, 0, ROWS>(A, m_next, c_next, W, wave, a, Vs, X, Y, st);
   AIY_EGM_STAMP(W, 3);
   __syncthreads();
   if (!TERMINAL && (int)threadIdx.x < ROWS * A.S) hints[(size_t)W.w * ROWS * A.S + threadIdx.x] = s_hint[threadIdx.x];
@@ -592,8 +633,10 @@ __global__ __launch_bounds__(kEgmBlock, (SC > 0 || SMAX <= 16) ? AIY_EGM_WAVES_P
   }
   if (false)
 #endif
-  if (log_util) dmax = egm_phase2<SMAX, SC, true>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
-  else dmax = egm_phase2<SMAX, SC, false>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
+  if (pk == 1) dmax = egm_phase2<SMAX, SC, 1>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
+  else if (pk == 3) dmax = egm_phase2<SMAX, SC, 3>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
+  else if (pk == 5) dmax = egm_phase2<SMAX, SC, 5>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
+  else dmax = egm_phase2<SMAX, SC, 0>(A, m_next, c_next, m_out, c_out, W, wave, ic, a, track, Vs, Pl, s_par);
 
   AIY_EGM_STAMP(W, 5);
   if (dist_slots != nullptr) {

@@ -298,21 +298,30 @@ __global__ __launch_bounds__(256) void hist_step_kernel(int S, int n_a, const in
   }
 }
 
-__global__ __launch_bounds__(256) void hist_K_kernel(int S, int n_a, const double* __restrict__ mass,
-                                                     const double* __restrict__ a_grid, double* __restrict__ K) {
+// K = sum_{s, j} mass[s][j] a_j per calibration (one 1024-thread block each): per node
+// the S masses summed in state order, times a_j, then a fixed-order block reduction.
+constexpr int kKThreads = 1024;
+__global__ __launch_bounds__(kKThreads) void hist_K_kernel(int S, int n_a, const double* __restrict__ mass,
+                                                           const double* __restrict__ a_grid,
+                                                           double* __restrict__ K) {
   const int cal = blockIdx.x;
   double acc = 0.0;
   const double* ag = a_grid + (size_t)cal * n_a;
   const double* mc = mass + (size_t)cal * S * n_a;
-  for (int idx = threadIdx.x; idx < S * n_a; idx += blockDim.x) acc += mc[idx] * ag[idx % n_a];
-  __shared__ double red[256];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+  for (int j = threadIdx.x; j < n_a; j += kKThreads) {
+    double ms = 0.0;
+    for (int s = 0; s < S; ++s) ms += mc[(size_t)s * n_a + j];
+    acc += ms * ag[j];
   }
-  if (threadIdx.x == 0) K[cal] = red[0];
+  __shared__ double red[kKThreads / kWave];
+  acc = wave_sum_fixed(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double k = 0.0;
+    for (int w = 0; w < kKThreads / kWave; ++w) k += red[w];
+    K[cal] = k;
+  }
 }
 
 static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
@@ -374,7 +383,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
       if (!e) AIY_HIP(h, hipEventCreate(&e));
     rc = hist_solve_resident(h, n_cal, S, n_a, lo, wlo, P, tol, max_iter, mass, h->d_hlast, st);
     if (rc == AIY_OK) {
-      hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(256), 0, st, S, n_a, mass, a_grid, h->d_K);
+      hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(kKThreads), 0, st, S, n_a, mass, a_grid, h->d_K);
       AIY_CHECK_LAUNCH(h);
       AIY_HIP(h, hipMemcpyAsync(h->h_hlast, h->d_hlast, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
       AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
@@ -455,7 +464,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
       AIY_HIP(h, hipMemcpyAsync(mass + off, alt + off, (size_t)S * n_a * sizeof(double), hipMemcpyDeviceToDevice, st));
     }
   }
-  hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(256), 0, st, S, n_a, mass, a_grid, h->d_K);
+  hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(kKThreads), 0, st, S, n_a, mass, a_grid, h->d_K);
   AIY_CHECK_LAUNCH(h);
   AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipStreamSynchronize(st));

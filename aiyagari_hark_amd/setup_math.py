@@ -9,7 +9,7 @@ Citations: AS = /root/reference/Aiyagari_Support.py, [HARK] = econ-ark 0.12.
 from __future__ import annotations
 
 import numpy as np
-from scipy import stats
+from scipy import special
 
 MGRID_BASE = np.array([0.1, 0.3, 0.6, 0.8, 0.9, 0.95, 0.98, 1.0, 1.02, 1.05, 1.1, 1.2, 1.6, 2.0, 3.0])
 
@@ -35,7 +35,7 @@ def tauchen(n, sigma, rho, bound=3.0):
     y = np.linspace(-top, top, n)
     d = y[1] - y[0]
     P = np.ones((n, n))
-    cdf = stats.norm.cdf
+    cdf = special.ndtr   # = stats.norm.cdf (scipy's norm._cdf is ndtr), without the per-call overhead
     for j in range(n):
         for k in range(1, n - 1):
             P[j, k] = cdf((y[k] + d / 2.0 - rho * y[j]) / sigma) - cdf((y[k] - d / 2.0 - rho * y[j]) / sigma)
