@@ -101,8 +101,24 @@ __global__ void fill_value_kernel(double* x, long long n, double v) {
   if (q < n) x[q] = v;
 }
 
+// Secant start of the next K_s(r) evaluation from the last two (per calibration):
+// x0 = cur + theta_c (cur - prev), theta_c = (r_next - r_cur) / (r_cur - r_prev) (clamped
+// to [-1, 1]; 0 without a history), over `per` values per calibration.  The household
+// solve and the distribution solve then start O(dr^2) from their fixed points instead of
+// O(dr); the fixed points, and the stopping rules that certify them, are unchanged.
+__global__ void secant_start_kernel(long long per, int n_cal, const double* __restrict__ theta,
+                                    const double* __restrict__ cur, const double* __restrict__ prev,
+                                    double* __restrict__ out) {
+  const long long n = per * n_cal;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+    const double th = theta[q / per];
+    const double c = cur[q];
+    out[q] = th == 0.0 ? c : c + th * (c - prev[q]);
+  }
+}
+
 struct GeLayout {
-  size_t Rn, Wn, Mn, Mg, Rc, wc, tm, tc, wm, wc2, lo, wlo, mass, hw, bytes;
+  size_t Rn, Wn, Mn, Mg, Rc, wc, tm, tc, wm, wc2, lo, wlo, mass, hw, pm, pc, im, ic, pmass, th, bytes;
 };
 static GeLayout ge_layout(int n_cal, int S, int n_a) {
   GeLayout L;
@@ -113,6 +129,8 @@ static GeLayout ge_layout(int n_cal, int S, int n_a) {
   L.Rc = take((size_t)n_cal * 8); L.wc = take((size_t)n_cal * 8);
   L.tm = take(tab * 8); L.tc = take(tab * 8); L.wm = take(2 * tab * 8); L.wc2 = take(2 * tab * 8);
   L.lo = take(pts * 4); L.wlo = take(pts * 8); L.mass = take(pts * 8); L.hw = take(2 * pts * 8);
+  L.pm = take(tab * 8); L.pc = take(tab * 8); L.im = take(tab * 8); L.ic = take(tab * 8);
+  L.pmass = take(pts * 8); L.th = take((size_t)n_cal * 8);
   L.bytes = o;
   return L;
 }
@@ -156,6 +174,15 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   double* wlo = reinterpret_cast<double*>(base + L.wlo);
   double* mass = reinterpret_cast<double*>(base + L.mass);
   double* hw = reinterpret_cast<double*>(base + L.hw);
+  double* pm = reinterpret_cast<double*>(base + L.pm);      // previous evaluation's tables
+  double* pc = reinterpret_cast<double*>(base + L.pc);
+  double* im = reinterpret_cast<double*>(base + L.im);      // secant starts
+  double* ic = reinterpret_cast<double*>(base + L.ic);
+  double* pmass = reinterpret_cast<double*>(base + L.pmass);
+  double* d_th = reinterpret_cast<double*>(base + L.th);
+  const long long tab_per = (long long)S * (n_a + 1), pts_per = (long long)S * n_a;
+  std::vector<double> r_cur(n_cal, 0.0), r_prev(n_cal, 0.0), theta(n_cal, 0.0);
+  const unsigned sec_blocks = 1024;
   AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
 
   std::vector<RootSearch> rs(n_cal);
@@ -190,9 +217,29 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
                        Mn);
     AIY_CHECK_LAUNCH(h);
     const bool warm_egm = o->warm_egm && steps > 0;
+    // secant starts (steps >= 2, warm): x0 = cur + theta (cur - prev); the current
+    // evaluation's tables / mass become the previous ones (pointer swap)
+    const bool secant = o->secant_start && o->warm_egm && o->warm_hist && steps >= 2;
+    if (secant) {
+      for (int c = 0; c < n_cal; ++c) {
+        const double den = r_cur[c] - r_prev[c];
+        double th = den != 0.0 ? (rs[c].x - r_cur[c]) / den : 0.0;
+        theta[c] = std::isfinite(th) ? std::max(-1.0, std::min(1.0, th)) : 0.0;
+      }
+      AIY_HIP(h, hipMemcpyAsync(d_th, theta.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(secant_start_kernel, dim3(sec_blocks), dim3(256), 0, st, tab_per, n_cal, d_th, tm, pm, im);
+      hipLaunchKernelGGL(secant_start_kernel, dim3(sec_blocks), dim3(256), 0, st, tab_per, n_cal, d_th, tc, pc, ic);
+      AIY_CHECK_LAUNCH(h);
+    }
+    if (warm_egm) {
+      std::swap(tm, pm);   // pm: the current evaluation's tables (next step's "previous")
+      std::swap(tc, pc);
+    }
+    const double* init_m = secant ? im : pm;
+    const double* init_c = secant ? ic : pc;
     rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, 32,
-                            warm_egm ? tm : nullptr, warm_egm ? tc : nullptr, wm, wc2, tm, tc, cyc.data(), dist.data(),
-                            stream);
+                            warm_egm ? init_m : nullptr, warm_egm ? init_c : nullptr, wm, wc2, tm, tc, cyc.data(),
+                            dist.data(), stream);
     if (rc) break;
     rc = aiy_hist_lottery(h, n_cal, S, n_a, tm, tc, M->a_grid, Rc, wc, M->lab, lo, wlo, stream);
     if (rc) break;
@@ -201,6 +248,18 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
       hipLaunchKernelGGL(fill_value_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, mass, n,
                          1.0 / ((double)S * n_a));
       AIY_CHECK_LAUNCH(h);
+    } else if (o->warm_egm) {
+      // mass <- secant start from (mass, pmass); pmass <- the current evaluation's mass
+      const size_t mb = sizeof(double) * pts_per * n_cal;
+      if (secant) {
+        hipLaunchKernelGGL(secant_start_kernel, dim3(sec_blocks), dim3(256), 0, st, pts_per, n_cal, d_th, mass, pmass,
+                           hw);
+        AIY_CHECK_LAUNCH(h);
+        std::swap(mass, pmass);
+        AIY_HIP(h, hipMemcpyAsync(mass, hw, mb, hipMemcpyDeviceToDevice, st));
+      } else {
+        AIY_HIP(h, hipMemcpyAsync(pmass, mass, mb, hipMemcpyDeviceToDevice, st));
+      }
     }
     h->hist_accel = o->accel > 0 ? o->accel : 0;   // accel < 0: BiCGSTAB (AIY_OPT_HIST_KRYLOV)
     h->hist_krylov = o->accel < 0;
@@ -212,6 +271,8 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     for (int c = 0; c < n_cal; ++c) {
       cyc_sum += cyc[c];
       it_sum += its[c];
+      r_prev[c] = r_cur[c];
+      r_cur[c] = rs[c].x;
       rs[c].update(Ks[c] - Kd[c]);
     }
     ++steps;

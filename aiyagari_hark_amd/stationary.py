@@ -241,7 +241,7 @@ class _Brent:
 
 
 def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo=None,
-                         r_hi=None):
+                         r_hi=None, secant=False):
     """The whole E1 search in ONE library call (aiy_ge_stationary: the bracket updates run
     in C++ between device K_s evaluations).  Returns (r, K, Ks, steps, egm_cycles_sum,
     hist_iters_sum)."""
@@ -259,7 +259,7 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
     opt = _lib.GeOptions({"bisect": 0, "brent": 1}[method], float(r_tol), float(egm_tol), float(hist_tol),
                          int(max_steps), 5000, 200000, int(bool(warm_hist)), int(bool(warm_egm)), int(accel),
                          ctypes.addressof(lo) if lo is not None else None,
-                         ctypes.addressof(hi) if hi is not None else None)
+                         ctypes.addressof(hi) if hi is not None else None, int(bool(secant)))
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
@@ -270,7 +270,7 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
 
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
-                 method="bisect", warm_egm=None, accel=None, engine="native"):
+                 method="bisect", warm_egm=None, accel=None, engine="native", secant=None):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -284,7 +284,11 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     BiCGSTAB for "brent", 0 = the plain iteration for "bisect"; E > 0: Aitken period) --
     the distribution solver (StationaryBatch.capital_supply).
     engine: "native" -- one aiy_ge_stationary call (C++ search loop); "python" -- the same
-    search driven from Python step by step (per-step logs; identical iterates)."""
+    search driven from Python step by step (per-step logs; identical iterates when
+    secant=False).  secant (native only; default: on for "brent"): from the third
+    evaluation on, the household and distribution solves start from the secant
+    extrapolation of the last two evaluations' solutions (same fixed points to the same
+    stopping rules, fewer cycles / matvecs)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     b = StationaryBatch(cals, aGrid, device=device)
@@ -299,10 +303,13 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     steps = 0
     cyc_log, it_log = [], []
     Ks = np.zeros(n)
+    if secant is None:
+        secant = method == "brent"
     if engine == "native" and log is None:
         r, K, Ks, steps, cyc_sum, it_sum = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
                                                                 warm_hist, warm_egm, accel, r_lo if r_lo is not None
-                                                                else None, r_hi if r_hi is not None else None)
+                                                                else None, r_hi if r_hi is not None else None,
+                                                                secant=secant and warm_hist and warm_egm)
         KtoY = K ** (1.0 - b.alpha)
         return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
                                 egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])])

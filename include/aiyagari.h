@@ -398,6 +398,11 @@ typedef struct {
   int32_t accel;         /* Aitken period of the distribution iteration (0: plain; < 0: BiCGSTAB) */
   const double* r_lo;    /* HOST [n_cal] or NULL: -delta / 2                                   */
   const double* r_hi;    /* HOST [n_cal] or NULL: 1 / beta - 1 - 1e-9                          */
+  int32_t secant_start;  /* != 0 (with warm_hist and warm_egm): from the third step on, each
+                            evaluation starts its household and distribution solves at
+                            cur + theta (cur - prev), theta = (r - r_cur) / (r_cur - r_prev)
+                            clamped to [-1, 1] (the fixed points and stopping rules are
+                            unchanged; iterates differ from the Python-driven loop)          */
 } aiy_ge_options;
 
 /* Device scratch the call needs (caller-owned `work`), -1 for bad sizes. */
