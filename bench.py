@@ -46,6 +46,10 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
 PANEL_BYTES_PER_AGENT = 18     # a in/out 16 B + labour state in/out 2 B (Philox)
 HIST_BYTES_PER_POINT = 28      # mass in 8, lottery index 4, weight 8, mass out 8
+# per (state, node) point and matvec of the BiCGSTAB distribution solve (hist_krylov.hip):
+# the 28 B of the push/mix matvec plus half an iteration's iterate traffic (x read and
+# written twice, p written and read: 48 B per iteration of two matvecs)
+HIST_BYTES_PER_POINT_KRYLOV = 52
 N_AGENTS = 1_000_006           # nearest multiple of 7 >= 1e6
 N_AGENTS_C3 = 99_999_998       # 1e8 agents, multiple of 7
 T_C3 = 1000
@@ -142,7 +146,7 @@ def table2_leg(args, world, rank, dev):
     for _ in range(args.warmup):
         sweep()
     hist_stats(h, True)
-    point_iters = 0
+    point_iters = 0   # (state, node) points x matvecs of the distribution solves
     res = None
     barrier(world)
     t0 = time.perf_counter()
@@ -152,9 +156,9 @@ def table2_leg(args, world, rank, dev):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     hist_ms, hist_n = hist_stats(h, True)
-    # dominant kernel: the device-resident distribution iteration (one launch per K_s(r)
-    # evaluation); algorithmic bytes 28 per (state, node) point per iteration
-    hist_bytes = HIST_BYTES_PER_POINT * point_iters
+    # dominant kernel: the device-resident BiCGSTAB distribution solve (one launch per K_s(r)
+    # evaluation); algorithmic bytes 52 per (state, node) point per matvec
+    hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
     hist_gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[float(x) for x in res.r], KtoY=[float(x) for x in res.KtoY],
                                    evaluations=res.bisection_steps), world)
@@ -528,14 +532,17 @@ def main():
                                "Young-lottery stationary distribution; one step = the whole sweep",
                    "calibrations": N_TABLE2, "n_a": args.grid, "S": 7,
                    "parallelism": f"calibrations split round-robin over {world} GPU(s), no data-path collective"},
-        "roofline": {"kernel": "hist_cluster_kernel (device-resident Young histogram)", "bound": "hbm",
+        "roofline": {"kernel": "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery "
+                               "stationary distribution)", "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("hist_cluster_kernel", scale=t2["hist_bytes_per_launch"] / 28.0),
+                     "traffic": pmc_traffic("hist_bicg_kernel",
+                                            scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV),
                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
                      "avg_launch_ms": t2["hist_avg_launch_ms"],
-                     "launch": "one K_s(r) evaluation of the rank's calibrations: every distribution iteration "
-                               "(28 B per state x node point per iteration)",
+                     "launch": "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
+                               "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
+                               "updates)",
                      "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"])},
         "table2": {k: t2[k] for k in ("seconds_per_sweep", "evaluations_rank0", "hist_launches_per_sweep",
                                       "hist_kernel_ms_per_sweep", "r_percent", "saving_rate_percent")},

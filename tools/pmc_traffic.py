@@ -1,6 +1,8 @@
 """Summarise rocprofv3 PMC passes into per-launch HBM traffic for bench.py.
 
-Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [bench_log]
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [bench_log] [kernel,kernel,...]
+(entries of other kernels are kept when <out.json> exists; the optional list restricts
+which kernels of these passes are taken, e.g. the Table II leg's hist_bicg_kernel only)
 
 With the log of the profiled bench run (its "hist_point_iters=" line), the device-resident
 histogram also gets hbm_bytes_per_point_iter: its launches differ in iteration count, so
@@ -56,10 +58,15 @@ def main():
         res[short] = dict(kernel=k, fetch_kb_raw=f_kb, write_kb=w_kb, dispatches=[nf, nw],
                           hbm_bytes_per_launch=(2.0 * f_kb + w_kb) * 1024.0,
                           correction="FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1")
-        if short == "hist_cluster_kernel" and pts > 0:
+        if short in ("hist_cluster_kernel", "hist_bicg_kernel") and pts > 0:
             res[short]["point_iters"] = pts
             res[short]["hbm_bytes_per_point_iter"] = (2.0 * f_kb * nf + w_kb * nw) * 1024.0 / pts
-    json.dump(res, open(out, "w"), indent=1)
+    merged = {}
+    if os.path.exists(out):   # keep the other kernels' entries (earlier passes of other legs)
+        merged = json.load(open(out))
+    only = sys.argv[5].split(",") if len(sys.argv) > 5 else None   # kernels to take from these passes
+    merged.update({k: v for k, v in res.items() if only is None or k in only})
+    json.dump(merged, open(out, "w"), indent=1)
     for k, v in res.items():
         print(f"{k}: {v['hbm_bytes_per_launch'] / 1e6:.2f} MB/launch (fetch raw {v['fetch_kb_raw']:.0f} KB, "
               f"write {v['write_kb']:.0f} KB)")
