@@ -103,6 +103,7 @@ struct EgmDev {
   const double* lab;
   const double* beta;
   const double* crra;
+  const double* tolv;   // per-calibration convergence tolerance (device) or null: the launch's tol
 };
 
 // XCD-aware work decode.  The grid is padded to a multiple of 8 and workgroups are
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(kEgmBlock, (SC > 0 || SMAX <= 16) ? AIY_EGM_WAVES_P
         d = __longlong_as_double((long long)load_u64_agent(&slots[((cycle - 1) % 3) * kSub + threadIdx.x]));
       d = wave_nan_max(d);
       if (threadIdx.x == 0) {
-        const bool skip = done || !(d > tol);
+        const bool skip = done || !(d > (A.tolv ? A.tolv[cal] : tol));
         s_skip = skip ? 1 : 0;
         if (skip && !done && lead) store_u64_agent(&slots[kFlag], 1ull);
       }
@@ -715,6 +716,7 @@ static EgmDev to_dev(const aiy_egm_dims* d, const aiy_egm_inputs* in) {
   A.n_cal = d->n_cal; A.S = d->S; A.n_M = d->n_M; A.n_a = d->n_a;
   A.a_grid = in->a_grid; A.M_grid = in->M_grid; A.P = in->P; A.R_next = in->R_next;
   A.W_next = in->W_next; A.M_next = in->M_next; A.lab = in->lab; A.beta = in->beta; A.crra = in->crra;
+  A.tolv = nullptr;
   return A;
 }
 
@@ -832,6 +834,8 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
   const size_t per_cal = (size_t)dims->S * dims->n_M * (dims->n_a + 1);
   const size_t buf = per_cal * n_cal;
   EgmDev A = to_dev(dims, in);
+  A.tolv = h->egm_tolv;   // per-calibration tolerances of aiy_ge_stationary, if set
+  auto tol_of = [&](int c) { return h->egm_tolh ? h->egm_tolh[c] : tol; };
   int* hints = nullptr;
   rc = egm_hints(h, A, st, &hints);
   if (rc) return rc;
@@ -861,7 +865,7 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
     for (int c = 0; c < n_cal; ++c) {
       const int last = h->h_last[c];
       const double d = slot_max(h->h_dist + (size_t)c * kSlots, last);
-      const bool conv = (last >= 2 && !(d > tol)) || last >= last_allowed;
+      const bool conv = (last >= 2 && !(d > tol_of(c))) || last >= last_allowed;
       all = all && conv;
     }
     next = end;

@@ -118,7 +118,7 @@ __global__ void secant_start_kernel(long long per, int n_cal, const double* __re
 }
 
 struct GeLayout {
-  size_t Rn, Wn, Mn, Mg, Rc, wc, tm, tc, wm, wc2, lo, wlo, mass, hw, pm, pc, im, ic, pmass, th, bytes;
+  size_t Rn, Wn, Mn, Mg, Rc, wc, tm, tc, wm, wc2, lo, wlo, mass, hw, pm, pc, im, ic, pmass, th, etol, htol, bytes;
 };
 static GeLayout ge_layout(int n_cal, int S, int n_a) {
   GeLayout L;
@@ -131,6 +131,7 @@ static GeLayout ge_layout(int n_cal, int S, int n_a) {
   L.lo = take(pts * 4); L.wlo = take(pts * 8); L.mass = take(pts * 8); L.hw = take(2 * pts * 8);
   L.pm = take(tab * 8); L.pc = take(tab * 8); L.im = take(tab * 8); L.ic = take(tab * 8);
   L.pmass = take(pts * 8); L.th = take((size_t)n_cal * 8);
+  L.etol = take((size_t)n_cal * 8); L.htol = take((size_t)n_cal * 8);
   L.bytes = o;
   return L;
 }
@@ -182,6 +183,15 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   double* d_th = reinterpret_cast<double*>(base + L.th);
   const long long tab_per = (long long)S * (n_a + 1), pts_per = (long long)S * n_a;
   std::vector<double> r_cur(n_cal, 0.0), r_prev(n_cal, 0.0), theta(n_cal, 0.0);
+  // loose bracketing: per-calibration tolerances of this step, and the calibrations whose
+  // last (loose) evaluation was too close to the root to trust its sign
+  double* d_etol = reinterpret_cast<double*>(base + L.etol);
+  double* d_htol = reinterpret_cast<double*>(base + L.htol);
+  std::vector<double> etol(n_cal, o->egm_tol), htol(n_cal, o->hist_tol);
+  std::vector<char> loose(n_cal, 0), refine(n_cal, 0);
+  const bool loose_on = o->loose_bracket && o->method == 1;
+  const double kLooseEgm = std::max(o->egm_tol, 1e-6), kLooseHist = std::max(o->hist_tol, 1e-10);
+  const double kSignMargin = 0.05;   // |K_s - K_d| / K_d that a loose evaluation's sign needs
   const unsigned sec_blocks = 1024;
   AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
 
@@ -216,6 +226,18 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     hipLaunchKernelGGL(fill_prices_kernel, dim3((n_cal * S + 255) / 256), dim3(256), 0, st, n_cal, S, Rc, wc, Rn, Wn,
                        Mn);
     AIY_CHECK_LAUNCH(h);
+    if (loose_on) {
+      for (int c = 0; c < n_cal; ++c) {
+        loose[c] = !rs[c].brent && !rs[c].done && !refine[c];
+        etol[c] = loose[c] ? kLooseEgm : o->egm_tol;
+        htol[c] = loose[c] ? kLooseHist : o->hist_tol;
+      }
+      AIY_HIP(h, hipMemcpyAsync(d_etol, etol.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+      AIY_HIP(h, hipMemcpyAsync(d_htol, htol.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+      h->egm_tolv = d_etol;
+      h->egm_tolh = etol.data();
+      h->hist_tolv = d_htol;
+    }
     const bool warm_egm = o->warm_egm && steps > 0;
     // secant starts (steps >= 2, warm): x0 = cur + theta (cur - prev); the current
     // evaluation's tables / mass become the previous ones (pointer swap)
@@ -240,7 +262,10 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, 32,
                             warm_egm ? init_m : nullptr, warm_egm ? init_c : nullptr, wm, wc2, tm, tc, cyc.data(),
                             dist.data(), stream);
-    if (rc) break;
+    if (rc) {
+      h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
+      break;
+    }
     rc = aiy_hist_lottery(h, n_cal, S, n_a, tm, tc, M->a_grid, Rc, wc, M->lab, lo, wlo, stream);
     if (rc) break;
     if (!(o->warm_hist && steps > 0)) {
@@ -267,18 +292,22 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
                         o->max_hist_iter > 0 ? o->max_hist_iter : 200000, 64, mass, hw, Ks.data(), its.data(), stream);
     h->hist_accel = saved_accel;
     h->hist_krylov = saved_krylov;
+    h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
     if (rc) break;
     for (int c = 0; c < n_cal; ++c) {
       cyc_sum += cyc[c];
       it_sum += its[c];
       r_prev[c] = r_cur[c];
       r_cur[c] = rs[c].x;
-      rs[c].update(Ks[c] - Kd[c]);
+      const double f = Ks[c] - Kd[c];
+      refine[c] = loose[c] && !(std::fabs(f) >= kSignMargin * Kd[c]);   // NaN: refine
+      if (!refine[c]) rs[c].update(f);
     }
     ++steps;
   }
   h->hist_accel = saved_accel;
   h->hist_krylov = saved_krylov;
+  h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
   if (rc) return rc;
   for (int c = 0; c < n_cal; ++c) {
     const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];

@@ -35,6 +35,7 @@ struct HcRun {
   int* iters_out;         // [n_cal]
   unsigned* err;          // 0 ok, 1 timeout, 2 span overflow / not monotone, 3 candidate overflow
   double tol;
+  const double* tolv;     // [n_cal] per-calibration tolerance (device) or null: tol
   int max_iter;
 };
 

@@ -52,13 +52,14 @@ __device__ __forceinline__ double hk_rhat(unsigned q) {
   return (double)(int)h * (1.0 / 2147483648.0);
 }
 
-// Phase timing (diagnostic builds, -DAIY_DIAG_PHASES=<block>): time since the previous
+// Phase timing (diagnostic builds, -DAIY_DIAG_PHASES=<block>: that block and the next 9,
+// i.e. one calibration's cluster at Table II size): time since the previous
 // mark is added to slot k: 0 push, 1 publish, 2 matvec barrier, 3 gather + mix,
 // 4 reductions (partials, publish, barrier, read), 5 vector updates
 #ifdef AIY_DIAG_PHASES
 #define HK_PH(k)                                                        \
   do {                                                                  \
-    if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES) {                    \
+    if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10) { \
       const unsigned long long tn = __builtin_amdgcn_s_memrealtime();   \
       if ((k) >= 0) ph[(k)] += tn - tq;                                 \
       tq = tn;                                                          \
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   double* Pg = r.dbuf + row0 * n_a;
   auto vidx = [&](int k, int s) { return (k * SMAX + s) * TH + tid; };
   double part[kHkRed];
-  const double tol = r.tol;
+  const double tol = r.tolv ? r.tolv[cal] : r.tol;
   int mv = 0;                 // matvecs
   bool restart = true, first = true;
   double rho = 0.0, total0 = 0.0;
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   }
   if (w == 0 && tid == 0) r.iters_out[cal] = mv;
 #ifdef AIY_DIAG_PHASES
-  if (tid == 0 && blockIdx.x == AIY_DIAG_PHASES && mv > 0)
+  if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10 && mv > 0)
     printf("[bicg phases] block %d G=%d nj=%d matvecs=%d us/matvec: push %.2f publish %.2f barrier %.2f gather+mix "
            "%.2f reduce %.2f vector %.2f\n",
            (int)blockIdx.x, G, r.nj, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv, ph[3] * 0.01 / mv,

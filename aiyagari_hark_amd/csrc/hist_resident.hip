@@ -630,6 +630,7 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   HcRun r;
   r.n_cal = n_cal; r.S = S; r.n_a = n_a; r.G = p.G; r.nj = p.nj; r.cap = p.cap;
   r.lo = lo; r.wlo = wlo; r.P = P; r.mass = mass; r.iters_out = d_iters; r.tol = tol; r.max_iter = max_iter;
+  r.tolv = krylov ? h->hist_tolv : nullptr;   // per-calibration tolerances (BiCGSTAB form)
   r.slab = reinterpret_cast<double*>(base);
   size_t off = (size_t)per_launch * p.G * 2 * p.cap * sizeof(double);
   r.span = reinterpret_cast<int*>(base + off);

@@ -42,6 +42,11 @@ struct aiy_handle {
   int hist_cluster_cap = 0;          // AIY_OPT_HIST_CLUSTER: max workgroups per calibration (0: 32)
   int hist_accel = 0;                // AIY_OPT_HIST_ACCEL: Aitken period of the resident histogram (0: off)
   int hist_krylov = 0;               // AIY_OPT_HIST_KRYLOV: resident histogram solves by BiCGSTAB
+  // per-calibration tolerances for one call (aiy_ge_stationary's loose bracketing); null: the
+  // scalar tolerance of the call.  Device arrays [n_cal]; egm_tolh: the host copy.
+  const double* egm_tolv = nullptr;
+  const double* egm_tolh = nullptr;
+  const double* hist_tolv = nullptr;
   void* d_hcd = nullptr;             // resident histogram: stored differences (Aitken)
   size_t hc_dcap = 0;
   void* d_hc = nullptr;              // resident histogram: slabs, spans, counters, distances

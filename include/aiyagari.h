@@ -403,6 +403,11 @@ typedef struct {
                             cur + theta (cur - prev), theta = (r - r_cur) / (r_cur - r_prev)
                             clamped to [-1, 1] (the fixed points and stopping rules are
                             unchanged; iterates differ from the Python-driven loop)          */
+  int32_t loose_bracket; /* != 0 (method 1): while a calibration's search is still bracketing
+                            (bisection before the first sign change) its evaluations run to
+                            the looser tolerances egm 1e-6 / hist 1e-10; the sign of
+                            K_s - K_d is taken only where |K_s - K_d| >= 5 % of K_d, else
+                            the same r is evaluated again at the full tolerances          */
 } aiy_ge_options;
 
 /* Device scratch the call needs (caller-owned `work`), -1 for bad sizes. */
