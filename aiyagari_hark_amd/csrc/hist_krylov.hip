@@ -39,6 +39,7 @@
 namespace aiy {
 
 constexpr int kHkRed = 8;   // partial sums per reduction (at most)
+constexpr int kHkStall = 96;   // matvecs without a 10 % residual gain that count as a stall
 static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   __shared__ int s_tot;
   __shared__ HcCand s_cand[SMAX][kHcCand];
   __shared__ int s_ncand[SMAX];
-  __shared__ int s_cinfo[KC * SMAX * TH];
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];   // cf | cn << 8 (cf, cn <= kHcCand): LDS for 25 states
   __shared__ double s_P[SMAX * SMAX];
   __shared__ double s_part[kHkRed][TH / kWave];
   __shared__ double s_res[kHkRed];
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
           }
         }
       }
-      s_cinfo[(k * SMAX + s) * TH + tid] = cf | (cn << 8);
+      s_cinfo[(k * SMAX + s) * TH + tid] = (unsigned short)(cf | (cn << 8));
     }
   }
   constexpr bool kLoReg = SMAX <= 8 && KC == 1;   // with two columns per thread the registers hold the Krylov vectors
@@ -491,7 +492,10 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   bool restart = true, first = true;
   double rho = 0.0, total0 = 0.0;
   auto own = [&](int jc, int k, int s) { return s < S && jc + k * TH < j1; };
-  auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH)); };
+  unsigned seed = 0;   // shadow-residual choice; a stagnating solve restarts with the next one
+  auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH) + seed * 0x5BD1E995u); };
+  double best = __builtin_inf();   // best recursive max|r| since the last restart, and when
+  int mv_best = 0;
   auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
   HK_PH(-1);
   while (true) {
@@ -579,6 +583,18 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
         }))
       return;
     if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
+      restart = true;
+      continue;
+    }
+    // stagnation (BiCGSTAB can stall for a particular shadow residual: one Table II cell
+    // sat at max|r| ~ 6e-5 with the first hash): no 10 % gain in kHkStall matvecs ->
+    // restart from the true residual with the next shadow residual
+    if (first || s_res[1] < 0.9 * best) {
+      best = first ? __builtin_inf() : s_res[1];
+      mv_best = mv;
+    } else if (mv - mv_best > kHkStall) {
+      ++seed;
+      best = __builtin_inf();
       restart = true;
       continue;
     }
