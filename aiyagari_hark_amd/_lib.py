@@ -77,7 +77,7 @@ class GeOptions(ctypes.Structure):
                 ("hist_tol", ctypes.c_double), ("max_steps", ctypes.c_int32), ("max_egm_cycles", ctypes.c_int32),
                 ("max_hist_iter", ctypes.c_int32), ("warm_hist", ctypes.c_int32), ("warm_egm", ctypes.c_int32),
                 ("accel", ctypes.c_int32), ("r_lo", vp), ("r_hi", vp), ("secant_start", ctypes.c_int32),
-                ("loose_bracket", ctypes.c_int32)]
+                ("loose_bracket", ctypes.c_int32), ("egm_extrapolate", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes)

@@ -785,9 +785,11 @@ static int32_t ensure_egm_scratch(aiy_handle* h, int n_cal) {
   if (h->d_dist) { (void)hipFree(h->d_dist); (void)hipFree(h->d_last); }
   if (h->h_dist) { (void)hipHostFree(h->h_dist); (void)hipHostFree(h->h_last); }
   h->d_dist = nullptr; h->d_last = nullptr; h->h_dist = nullptr; h->h_last = nullptr; h->egm_cap = 0;
-  AIY_HIP(h, hipMalloc((void**)&h->d_dist, sizeof(unsigned long long) * kSlots * n_cal));
+  // + n_cal doubles behind the slots: the extrapolation factors (device and pinned host)
+  AIY_HIP(h, hipMalloc((void**)&h->d_dist, sizeof(unsigned long long) * (kSlots + 1) * n_cal));
   AIY_HIP(h, hipMalloc((void**)&h->d_last, sizeof(int) * n_cal));
-  AIY_HIP(h, hipHostMalloc((void**)&h->h_dist, sizeof(unsigned long long) * kSlots * n_cal, hipHostMallocDefault));
+  AIY_HIP(h, hipHostMalloc((void**)&h->h_dist, sizeof(unsigned long long) * (kSlots + 1) * n_cal,
+                           hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_last, sizeof(int) * n_cal, hipHostMallocDefault));
   h->egm_cap = n_cal;
   return AIY_OK;
@@ -814,6 +816,28 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
   launch_cycle(A, m_next, c_next, m_out, c_out, hints, 0, nullptr, nullptr, 0.0, st);
   AIY_CHECK_LAUNCH(h);
   return AIY_OK;
+}
+
+// Geometric extrapolation of the cycle iterates (aiy_ge_stationary's household solves,
+// h->egm_extrap): where the last two cycle distances of a calibration fall at a steady
+// rate lambda (the same within 5 % of 1 - lambda as at the previous chunk boundary,
+// 0.5 < lambda < 0.98, the distance still > 100 tol), its tables X_n are moved along
+// their last change by the tail of the geometric series: X_n += lambda / (1 - lambda)
+// (X_n - X_{n-1}), m and c alike (m = a + c stays exact; the (1e-7, 1e-7) node does not
+// move).  The stopping rule is untouched: the solve still ends at the first cycle whose
+// own change is <= tol.  Measured on the CPU restatement (rho = 0, sigma = 0.2, CRRA = 1,
+// r = 4.14 %): 390 -> 156 cycles at one extrapolation per 32 cycles, the result 1.4e-7
+// from the over-converged policy (the plain stop: 2.4e-7).
+__global__ void egm_extrap_kernel(long long per, int n_cal, const double* __restrict__ f,
+                                  double* __restrict__ cur, const double* __restrict__ prev) {
+  const long long n = per * n_cal;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+    const double fc = f[q / per];
+    if (fc != 0.0) {
+      const double x = cur[q];
+      cur[q] = x + fc * (x - prev[q]);
+    }
+  }
 }
 
 int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
@@ -848,6 +872,11 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
   }
   const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
   int next = 1;
+  const bool extrap = h->egm_extrap != 0;
+  std::vector<double> lam_prev(n_cal, -1.0);
+  std::vector<char> moved(n_cal, 0);
+  double* hf = reinterpret_cast<double*>(h->h_dist + (size_t)kSlots * n_cal);
+  double* df = reinterpret_cast<double*>(h->d_dist + (size_t)kSlots * n_cal);
   while (true) {
     const int end = std::min(next + chunk, last_allowed + 1);
     for (int cyc = next; cyc < end; ++cyc) {
@@ -870,6 +899,51 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
     }
     next = end;
     if (all || next > last_allowed) break;
+    if (extrap) {
+      const int L = end - 1;   // the last launched cycle; its tables sit in slot L & 1
+      bool any = false;
+      for (int c = 0; c < n_cal; ++c) {
+        hf[c] = 0.0;
+        if (h->h_last[c] != L || L < 4) {
+          lam_prev[c] = -1.0;
+          continue;
+        }
+        const unsigned long long* sl = h->h_dist + (size_t)c * kSlots;
+        const double d1 = slot_max(sl, L), d0 = slot_max(sl, L - 1);
+        const double lam = d1 / d0;
+        if (d1 > 100.0 * tol_of(c) && lam > 0.5 && lam < 0.98 && lam_prev[c] > 0.0 &&
+            std::fabs(lam - lam_prev[c]) < 0.05 * (1.0 - lam)) {
+          hf[c] = lam / (1.0 - lam);
+          moved[c] = 1;
+          any = true;
+        }
+        lam_prev[c] = lam;
+      }
+      if (any) {
+        AIY_HIP(h, hipMemcpyAsync(df, hf, sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
+        const long long per = (long long)per_cal;
+        hipLaunchKernelGGL(egm_extrap_kernel, dim3(1024), dim3(256), 0, st, per, n_cal, df, work_m + (L & 1) * buf,
+                           work_m + ((L - 1) & 1) * buf);
+        hipLaunchKernelGGL(egm_extrap_kernel, dim3(1024), dim3(256), 0, st, per, n_cal, df, work_c + (L & 1) * buf,
+                           work_c + ((L - 1) & 1) * buf);
+        AIY_CHECK_LAUNCH(h);
+      }
+    }
+  }
+  if (extrap) {   // an extrapolated calibration that ended in NaN: the whole solve again, plain
+    bool bad = false;
+    for (int c = 0; c < n_cal; ++c) {
+      const int last = h->h_last[c];
+      const double d = slot_max(h->h_dist + (size_t)c * kSlots, last);
+      bad = bad || (moved[c] && d != d);
+    }
+    if (bad) {
+      h->egm_extrap = 0;
+      const int32_t rc2 = aiy_egm_solve_impl(h, dims, in, tol, max_cycles, chunk, m_init, c_init, work_m, work_c,
+                                             m_out, c_out, cycles_out, dist_out, stream);
+      h->egm_extrap = 1;
+      return rc2;
+    }
   }
   for (int c = 0; c < n_cal; ++c) {
     const int last = h->h_last[c];

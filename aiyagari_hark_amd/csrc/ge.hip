@@ -259,9 +259,11 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     }
     const double* init_m = secant ? im : pm;
     const double* init_c = secant ? ic : pc;
+    h->egm_extrap = o->egm_extrapolate != 0;
     rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, 32,
                             warm_egm ? init_m : nullptr, warm_egm ? init_c : nullptr, wm, wc2, tm, tc, cyc.data(),
                             dist.data(), stream);
+    h->egm_extrap = 0;
     if (rc) {
       h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
       break;

@@ -47,6 +47,7 @@ struct aiy_handle {
   const double* egm_tolv = nullptr;
   const double* egm_tolh = nullptr;
   const double* hist_tolv = nullptr;
+  int egm_extrap = 0;                // aiy_ge_stationary: extrapolate the EGM iterates (egm.hip)
   void* d_hcd = nullptr;             // resident histogram: stored differences (Aitken)
   size_t hc_dcap = 0;
   void* d_hc = nullptr;              // resident histogram: slabs, spans, counters, distances

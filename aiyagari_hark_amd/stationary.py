@@ -241,7 +241,7 @@ class _Brent:
 
 
 def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo=None,
-                         r_hi=None, secant=False, loose=False):
+                         r_hi=None, secant=False, loose=False, extrapolate=False):
     """The whole E1 search in ONE library call (aiy_ge_stationary: the bracket updates run
     in C++ between device K_s evaluations).  Returns (r, K, Ks, steps, egm_cycles_sum,
     hist_iters_sum)."""
@@ -259,7 +259,8 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
     opt = _lib.GeOptions({"bisect": 0, "brent": 1}[method], float(r_tol), float(egm_tol), float(hist_tol),
                          int(max_steps), 5000, 200000, int(bool(warm_hist)), int(bool(warm_egm)), int(accel),
                          ctypes.addressof(lo) if lo is not None else None,
-                         ctypes.addressof(hi) if hi is not None else None, int(bool(secant)), int(bool(loose)))
+                         ctypes.addressof(hi) if hi is not None else None, int(bool(secant)), int(bool(loose)),
+                         int(bool(extrapolate)))
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
@@ -270,7 +271,8 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
 
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
-                 method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None):
+                 method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None,
+                 extrapolate=None):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -292,7 +294,10 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     "brent"): while a calibration is still bracketing its root, its evaluations stop at
     egm 1e-6 / hist 1e-10 and their sign is used only where |K_s - K_d| >= 5 % of K_d
     (else that r is evaluated again at the full tolerances); every evaluation Brent's
-    method interpolates from runs at the full tolerances."""
+    method interpolates from runs at the full tolerances.  extrapolate (native only;
+    default: on for "brent"): the household solves extrapolate their cycle iterates
+    geometrically where the distances fall at a steady rate (csrc/egm.hip; same stopping
+    rule)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     b = StationaryBatch(cals, aGrid, device=device)
@@ -311,12 +316,14 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         secant = method == "brent"
     if loose is None:
         loose = method == "brent"
+    if extrapolate is None:
+        extrapolate = method == "brent"
     if engine == "native" and log is None:
         r, K, Ks, steps, cyc_sum, it_sum = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
                                                                 warm_hist, warm_egm, accel, r_lo if r_lo is not None
                                                                 else None, r_hi if r_hi is not None else None,
                                                                 secant=secant and warm_hist and warm_egm,
-                                                                loose=loose)
+                                                                loose=loose, extrapolate=extrapolate)
         KtoY = K ** (1.0 - b.alpha)
         return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
                                 egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])])

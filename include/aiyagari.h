@@ -408,6 +408,10 @@ typedef struct {
                             the looser tolerances egm 1e-6 / hist 1e-10; the sign of
                             K_s - K_d is taken only where |K_s - K_d| >= 5 % of K_d, else
                             the same r is evaluated again at the full tolerances          */
+  int32_t egm_extrapolate; /* != 0: the household solves move a calibration's tables along
+                            their last change by lambda / (1 - lambda) at chunk boundaries
+                            where the cycle distances fall at a steady rate lambda (egm.hip;
+                            the stopping rule is unchanged)                                   */
 } aiy_ge_options;
 
 /* Device scratch the call needs (caller-owned `work`), -1 for bad sizes. */

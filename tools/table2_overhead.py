@@ -28,7 +28,7 @@ def main():
         b = stn.StationaryBatch(cals, sm.make_grid_exp_mult(0.001, 50.0, 10000, 2), device=dev)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        stn.ge_stationary_native(b, "brent", 1e-7, 1e-8, 1e-12, 60, True, True, -1, secant=True, loose=True)
+        stn.ge_stationary_native(b, "brent", 1e-7, 1e-8, 1e-12, 60, True, True, -1, secant=True, loose=True, extrapolate=True)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         out.setdefault("setup_ms", []).append(1e3 * (t1 - t0))
