@@ -820,14 +820,14 @@ extern "C" int32_t aiy_egm_step(aiy_handle* h, const aiy_egm_dims* dims, const a
 
 // Geometric extrapolation of the cycle iterates (aiy_ge_stationary's household solves,
 // h->egm_extrap): where the last two cycle distances of a calibration fall at a steady
-// rate lambda (the same within 5 % of 1 - lambda as at the previous chunk boundary,
-// 0.5 < lambda < 0.98, the distance still > 100 tol), its tables X_n are moved along
+// rate lambda (the same within 20 % of 1 - lambda as at the previous chunk boundary,
+// 0.5 < lambda < 0.999, the distance still > 100 tol), its tables X_n are moved along
 // their last change by the tail of the geometric series: X_n += lambda / (1 - lambda)
 // (X_n - X_{n-1}), m and c alike (m = a + c stays exact; the (1e-7, 1e-7) node does not
 // move).  The stopping rule is untouched: the solve still ends at the first cycle whose
 // own change is <= tol.  Measured on the CPU restatement (rho = 0, sigma = 0.2, CRRA = 1,
-// r = 4.14 %): 390 -> 156 cycles at one extrapolation per 32 cycles, the result 1.4e-7
-// from the over-converged policy (the plain stop: 2.4e-7).
+// r = 4.14 %, cold): 390 -> 190 cycles with this rule at 32-cycle chunks; an
+// accelerated solve ends 1.4e-7 from the over-converged policy (the plain stop: 2.4e-7).
 __global__ void egm_extrap_kernel(long long per, int n_cal, const double* __restrict__ f,
                                   double* __restrict__ cur, const double* __restrict__ prev) {
   const long long n = per * n_cal;
@@ -911,8 +911,8 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
         const unsigned long long* sl = h->h_dist + (size_t)c * kSlots;
         const double d1 = slot_max(sl, L), d0 = slot_max(sl, L - 1);
         const double lam = d1 / d0;
-        if (d1 > 100.0 * tol_of(c) && lam > 0.5 && lam < 0.98 && lam_prev[c] > 0.0 &&
-            std::fabs(lam - lam_prev[c]) < 0.05 * (1.0 - lam)) {
+        if (d1 > 100.0 * tol_of(c) && lam > 0.5 && lam < 0.999 && lam_prev[c] > 0.0 &&
+            std::fabs(lam - lam_prev[c]) < 0.2 * (1.0 - lam)) {
           hf[c] = lam / (1.0 - lam);
           moved[c] = 1;
           any = true;
