@@ -21,6 +21,13 @@
 
 namespace aiy {
 
+// EGM cycles launched between two host checks of the household solves (convergence,
+// extrapolation); tuning builds override it
+#ifndef AIY_GE_EGM_CHUNK
+#define AIY_GE_EGM_CHUNK 32
+#endif
+constexpr int kGeEgmChunk = AIY_GE_EGM_CHUNK;
+
 // one calibration's root search (bisect-to-a-sign-change, then brentq)
 struct RootSearch {
   double lo, hi, xtol;
@@ -260,7 +267,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     const double* init_m = secant ? im : pm;
     const double* init_c = secant ? ic : pc;
     h->egm_extrap = o->egm_extrapolate != 0;
-    rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, 32,
+    rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, kGeEgmChunk,
                             warm_egm ? init_m : nullptr, warm_egm ? init_c : nullptr, wm, wc2, tm, tc, cyc.data(),
                             dist.data(), stream);
     h->egm_extrap = 0;
