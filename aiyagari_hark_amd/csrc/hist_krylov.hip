@@ -39,7 +39,7 @@
 namespace aiy {
 
 constexpr int kHkRed = 8;   // partial sums per reduction (at most)
-constexpr int kHkStall = 96;   // matvecs without a 10 % residual gain that count as a stall
+constexpr int kHkStall = 256;   // matvecs without a 10 % residual gain that count as a stall
 static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
