@@ -241,12 +241,13 @@ class _Brent:
 
 
 def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo=None,
-                         r_hi=None, secant=False, loose=False, extrapolate=False):
+                         r_hi=None, secant=False, loose=False, extrapolate=False, handle=None, stream=None):
     """The whole E1 search in ONE library call (aiy_ge_stationary: the bracket updates run
     in C++ between device K_s evaluations).  Returns (r, K, Ks, steps, egm_cycles_sum,
-    hist_iters_sum)."""
+    hist_iters_sum).  handle / stream: a library handle and torch stream of the caller's
+    (default: the device's shared handle, the current stream)."""
     n = len(b.cals)
-    h = _lib.handle(b.device.index)
+    h = handle if handle is not None else _lib.handle(b.device.index)
     work = torch.empty(int(h.lib.aiy_ge_stationary_work_bytes(n, b.S, b.n_a)), dtype=torch.uint8, device=b.device)
     host = lambda x: (ctypes.c_double * n)(*[float(v) for v in x])  # noqa: E731
     alpha, delta = host(b.alpha), host(b.delta)
@@ -264,15 +265,68 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
-                                    ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its), _lib.stream_ptr()),
+                                    ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its),
+                                    _lib.stream_ptr(stream)),
             "aiy_ge_stationary")
     return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value))
+
+
+_GROUP_CTX = {}   # (device, group) -> (library handle, torch stream), reused across sweeps
+
+
+def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel,
+                  r_lo, r_hi, secant, loose, extrapolate):
+    """Independent root searches for `groups` subsets of the calibrations, each on its own
+    library handle and stream from its own host thread (the library releases the GIL):
+    a batched search steps all its calibrations together and pays, at every step, for its
+    slowest one; decoupled groups do not wait for each other's slow steps.  Every group's
+    clusters must be co-resident with the others', so each calibration's cluster is capped
+    at (compute units / calibrations) workgroups (and 32)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(cals)
+    idx = [list(range(g, n, groups)) for g in range(groups)]
+    idx = [i for i in idx if i]
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    cap = max(1, min(32, cus // n))
+    cur = torch.cuda.current_stream(dev)
+    jobs = []
+    for gi, ii in enumerate(idx):
+        key = (dev.index, gi)
+        if key not in _GROUP_CTX:
+            _GROUP_CTX[key] = (_lib.Handle(dev.index), torch.cuda.Stream(dev))
+        h, st = _GROUP_CTX[key]
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, cap), "aiy_set_option")
+        b = StationaryBatch([cals[i] for i in ii], aGrid, device=dev)
+        sub = lambda x: None if x is None else np.broadcast_to(np.asarray(x, float), (n,))[ii]  # noqa: E731
+        st.wait_stream(cur)
+        jobs.append((ii, b, h, st, sub(r_lo), sub(r_hi)))
+
+    def run(job):
+        ii, b, h, st, lo, hi = job
+        with torch.cuda.stream(st):
+            return ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel,
+                                        lo, hi, secant=secant, loose=loose, extrapolate=extrapolate, handle=h,
+                                        stream=st)
+    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        outs = list(ex.map(run, jobs))
+    for _, _, _, st, _, _ in jobs:
+        cur.wait_stream(st)
+    r, K, Ks = np.zeros(n), np.zeros(n), np.zeros(n)
+    steps = cyc = its = 0
+    for (ii, b, *_), (rg, Kg, Ksg, sg, cg, ig) in zip(jobs, outs):
+        r[ii], K[ii], Ks[ii] = rg, Kg, Ksg
+        steps, cyc, its = max(steps, sg), cyc + cg, its + ig
+    alpha = np.array([c.CapShare for c in cals])
+    delta = np.array([c.DeprFac for c in cals])
+    KtoY = K ** (1.0 - alpha)
+    return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=delta * KtoY, bisection_steps=steps,
+                            egm_cycles=[np.array([cyc])], hist_iters=[np.array([its])])
 
 
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
                  method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None,
-                 extrapolate=None):
+                 extrapolate=None, groups=1):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -297,27 +351,32 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     method interpolates from runs at the full tolerances.  extrapolate (native only;
     default: on for "brent"): the household solves extrapolate their cycle iterates
     geometrically where the distances fall at a steady rate (csrc/egm.hip; same stopping
-    rule)."""
+    rule).  groups (native only): the calibrations split round-robin into independent
+    searches on their own handles, streams and host threads (_solve_groups)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
-    b = StationaryBatch(cals, aGrid, device=device)
-    n = len(cals)
-    lo = np.full(n, -0.5 * b.delta) if r_lo is None else np.broadcast_to(np.asarray(r_lo, float), (n,)).copy()
-    hi = (1.0 / np.array([c.DiscFac for c in cals]) - 1.0 - 1e-9) if r_hi is None else \
-        np.broadcast_to(np.asarray(r_hi, float), (n,)).copy()
     if warm_egm is None:
         warm_egm = method == "brent"
     if accel is None:
         accel = -1 if method == "brent" else 0
-    steps = 0
-    cyc_log, it_log = [], []
-    Ks = np.zeros(n)
     if secant is None:
         secant = method == "brent"
     if loose is None:
         loose = method == "brent"
     if extrapolate is None:
         extrapolate = method == "brent"
+    if engine == "native" and log is None and groups > 1 and len(cals) > 1:
+        return _solve_groups(cals, aGrid, torch.device(device or "cuda"), int(groups), method, r_tol, egm_tol,
+                             hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo, r_hi,
+                             secant and warm_hist and warm_egm, loose, extrapolate)
+    b = StationaryBatch(cals, aGrid, device=device)
+    n = len(cals)
+    lo = np.full(n, -0.5 * b.delta) if r_lo is None else np.broadcast_to(np.asarray(r_lo, float), (n,)).copy()
+    hi = (1.0 / np.array([c.DiscFac for c in cals]) - 1.0 - 1e-9) if r_hi is None else \
+        np.broadcast_to(np.asarray(r_hi, float), (n,)).copy()
+    steps = 0
+    cyc_log, it_log = [], []
+    Ks = np.zeros(n)
     if engine == "native" and log is None:
         r, K, Ks, steps, cyc_sum, it_sum = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
                                                                 warm_hist, warm_egm, accel, r_lo if r_lo is not None
