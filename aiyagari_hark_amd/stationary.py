@@ -326,7 +326,7 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
                  method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None,
-                 extrapolate=None, groups=1):
+                 extrapolate=None, groups=None):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -351,8 +351,10 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     method interpolates from runs at the full tolerances.  extrapolate (native only;
     default: on for "brent"): the household solves extrapolate their cycle iterates
     geometrically where the distances fall at a steady rate (csrc/egm.hip; same stopping
-    rule).  groups (native only): the calibrations split round-robin into independent
-    searches on their own handles, streams and host threads (_solve_groups)."""
+    rule).  groups (native only; default: 3 for "brent" with >= 3 calibrations, else 1):
+    the calibrations split round-robin into independent searches on their own handles,
+    streams and host threads (_solve_groups; 3 groups fill the process's hardware queues
+    beside the default stream -- 4 measured slower)."""
     cals = table2_calibrations() if cals is None else list(cals)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     if warm_egm is None:
@@ -365,6 +367,8 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         loose = method == "brent"
     if extrapolate is None:
         extrapolate = method == "brent"
+    if groups is None:
+        groups = 3 if (method == "brent" and engine == "native" and log is None and len(cals) >= 3) else 1
     if engine == "native" and log is None and groups > 1 and len(cals) > 1:
         return _solve_groups(cals, aGrid, torch.device(device or "cuda"), int(groups), method, r_tol, egm_tol,
                              hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo, r_hi,

@@ -122,10 +122,19 @@ def gather_objects(obj, world):
     return out
 
 
-def hist_stats(h, reset):
-    ms, n = ctypes.c_double(), ctypes.c_int64()
-    h.check(h.lib.aiy_hist_launch_stats(h.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "hist stats")
-    return ms.value, n.value
+def hist_stats(h, reset, dev=None):
+    """Resident-histogram kernel milliseconds and launches since the last reset, summed
+    over the device's shared handle and the handles of solve_table2's independent groups
+    (stationary._GROUP_CTX): per-launch HIP events, so overlapping groups are counted launch
+    by launch."""
+    from aiyagari_hark_amd import stationary
+    hs = [h] + [hg for (d, _), (hg, _) in stationary._GROUP_CTX.items() if dev is None or d == dev.index]
+    tot_ms, tot_n = 0.0, 0
+    for hh in hs:
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        hh.check(hh.lib.aiy_hist_launch_stats(hh.h, ctypes.byref(ms), ctypes.byref(n), int(reset)), "hist stats")
+        tot_ms, tot_n = tot_ms + ms.value, tot_n + n.value
+    return tot_ms, tot_n
 
 
 # ------------------------------------------------------------------------------------
@@ -145,7 +154,7 @@ def table2_leg(args, world, rank, dev):
 
     for _ in range(args.warmup):
         sweep()
-    hist_stats(h, True)
+    hist_stats(h, True, dev)
     point_iters = 0   # (state, node) points x matvecs of the distribution solves
     res = None
     barrier(world)
@@ -155,7 +164,7 @@ def table2_leg(args, world, rank, dev):
         point_iters += sum(int(np.sum(it)) for it in res.hist_iters) * 7 * args.grid
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
-    hist_ms, hist_n = hist_stats(h, True)
+    hist_ms, hist_n = hist_stats(h, True, dev)
     # dominant kernel: the device-resident BiCGSTAB distribution solve (one launch per K_s(r)
     # evaluation); algorithmic bytes 52 per (state, node) point per matvec
     hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
@@ -531,7 +540,8 @@ def main():
                                f"Aiyagari GE in r (Brent on K_s = K_d), {args.grid}-pt asset grid, 7-state Tauchen, "
                                "Young-lottery stationary distribution; one step = the whole sweep",
                    "calibrations": N_TABLE2, "n_a": args.grid, "S": 7,
-                   "parallelism": f"calibrations split round-robin over {world} GPU(s), no data-path collective"},
+                   "parallelism": f"calibrations split round-robin over {world} GPU(s), no data-path collective; "
+                                  "per GPU 3 independent root searches (own handle, stream, host thread)"},
         "roofline": {"kernel": "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery "
                                "stationary distribution)", "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -626,13 +626,14 @@ def test_native_ge_search_equals_python_loop(gpu, method):
     cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0),
             Calibration(LaborAR=0.3, LaborSD=0.4, CRRA=3.0)]
     nat = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="native", secant=False,
-                       loose=False, extrapolate=False)
+                       loose=False, extrapolate=False, groups=1)
     py = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="python")
     assert nat.bisection_steps == py.bisection_steps
     assert np.array_equal(nat.r, py.r)
     assert np.array_equal(nat.KtoY, py.KtoY)
     if method == "brent":   # secant starts: other iterates, the same root to the search tolerance
-        for sec_on, loose_on, ex_on in ((True, False, False), (True, True, False), (True, True, True)):
+        for sec_on, loose_on, ex_on, grp in ((True, False, False, 1), (True, True, False, 1), (True, True, True, 1),
+                                             (True, True, True, 3)):
             sec = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="native",
-                               secant=sec_on, loose=loose_on, extrapolate=ex_on)
-            assert np.max(np.abs(sec.r - py.r)) < 1e-7, (sec_on, loose_on, ex_on, np.abs(sec.r - py.r))
+                               secant=sec_on, loose=loose_on, extrapolate=ex_on, groups=grp)
+            assert np.max(np.abs(sec.r - py.r)) < 1e-7, (sec_on, loose_on, ex_on, grp, np.abs(sec.r - py.r))
