@@ -285,8 +285,8 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
     from concurrent.futures import ThreadPoolExecutor
     n = len(cals)
     # round-robin: on the Table II order this groups the cells by CRRA, i.e. cells whose
-    # slow steps coincide (dealing them in snake order, which mixes slow and fast cells in
-    # every group, measured 177 vs 204 GE solves/s)
+    # slow steps coincide (snake order, which mixes slow and fast cells in every group,
+    # measured 177 GE solves/s, contiguous (sigma, rho) blocks 176, round-robin 204)
     idx = [list(range(g, n, groups)) for g in range(groups)]
     idx = [i for i in idx if i]
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
