@@ -19,6 +19,7 @@ host only moves the brackets.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 from dataclasses import dataclass, field
 
@@ -272,6 +273,16 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
 
 
 _GROUP_CTX = {}   # (device, group) -> (library handle, torch stream), reused across sweeps
+
+
+def _close_groups():
+    """Destroy the group handles while the HIP runtime is up (as _lib.close_all does)."""
+    while _GROUP_CTX:
+        _, (h, _) = _GROUP_CTX.popitem()
+        h.close()
+
+
+atexit.register(_close_groups)
 
 
 def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel,
