@@ -383,6 +383,15 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         extrapolate = method == "brent"
     if groups is None:
         groups = 3 if (method == "brent" and engine == "native" and log is None and len(cals) >= 3) else 1
+    if groups > 1:
+        # concurrent groups need every calibration's cluster resident at once: the smallest
+        # cluster the grid allows (512-thread workgroups, 2 columns per thread for S <= 8)
+        # times the calibrations must fit the compute units, else one batched search
+        S0 = cals[0].LaborStatesNo
+        g_min = -(-n_a // (512 * (2 if S0 <= 8 else 1)))
+        cus = torch.cuda.get_device_properties(torch.device(device or "cuda")).multi_processor_count
+        if g_min * len(cals) > cus:
+            groups = 1
     if engine == "native" and log is None and groups > 1 and len(cals) > 1:
         return _solve_groups(cals, aGrid, torch.device(device or "cuda"), int(groups), method, r_tol, egm_tol,
                              hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo, r_hi,
