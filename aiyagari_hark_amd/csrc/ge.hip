@@ -27,6 +27,13 @@ namespace aiy {
 #define AIY_GE_EGM_CHUNK 32
 #endif
 constexpr int kGeEgmChunk = AIY_GE_EGM_CHUNK;
+// tolerances of the loose-bracketing evaluations (aiy_ge_options.loose_bracket)
+#ifndef AIY_GE_LOOSE_EGM
+#define AIY_GE_LOOSE_EGM 1e-6
+#endif
+#ifndef AIY_GE_LOOSE_HIST
+#define AIY_GE_LOOSE_HIST 1e-10
+#endif
 
 // one calibration's root search (bisect-to-a-sign-change, then brentq)
 struct RootSearch {
@@ -197,7 +204,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   std::vector<double> etol(n_cal, o->egm_tol), htol(n_cal, o->hist_tol);
   std::vector<char> loose(n_cal, 0), refine(n_cal, 0);
   const bool loose_on = o->loose_bracket && o->method == 1;
-  const double kLooseEgm = std::max(o->egm_tol, 1e-6), kLooseHist = std::max(o->hist_tol, 1e-10);
+  const double kLooseEgm = std::max(o->egm_tol, AIY_GE_LOOSE_EGM), kLooseHist = std::max(o->hist_tol, AIY_GE_LOOSE_HIST);
   const double kSignMargin = 0.05;   // |K_s - K_d| / K_d that a loose evaluation's sign needs
   const unsigned sec_blocks = 1024;
   AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
