@@ -35,6 +35,8 @@ AIY_OPT_HIST_RESIDENT = 6
 AIY_OPT_HIST_CLUSTER = 7
 AIY_OPT_HIST_ACCEL = 8
 AIY_OPT_HIST_KRYLOV = 9
+AIY_OPT_GE_RESIDENT = 10
+AIY_OPT_CU_LIMIT = 11
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -77,7 +79,7 @@ class GeOptions(ctypes.Structure):
                 ("hist_tol", ctypes.c_double), ("max_steps", ctypes.c_int32), ("max_egm_cycles", ctypes.c_int32),
                 ("max_hist_iter", ctypes.c_int32), ("warm_hist", ctypes.c_int32), ("warm_egm", ctypes.c_int32),
                 ("accel", ctypes.c_int32), ("r_lo", vp), ("r_hi", vp), ("secant_start", ctypes.c_int32),
-                ("loose_bracket", ctypes.c_int32), ("egm_extrapolate", ctypes.c_int32)]
+                ("loose_bracket", ctypes.c_int32), ("egm_extrapolate", ctypes.c_int32), ("status_out", vp)]
 
 
 # name -> (restype, argtypes)
@@ -137,6 +139,9 @@ SIGNATURES = {
                                         ctypes.c_double, ctypes.c_int32, ctypes.c_int32, vp, vp, c_double_p,
                                         c_int32_p, vp]),
     "aiy_hist_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
+    "aiy_ge_resident_plan": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_int32_p]),
+    "aiy_ge_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), c_double_p, c_double_p,
+                                             ctypes.c_int32]),
     "aiy_ge_stationary_work_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "aiy_ge_stationary": (ctypes.c_int32, [vp, ctypes.POINTER(StationaryModel), ctypes.POINTER(GeOptions), vp,
                                            c_double_p, c_double_p, c_double_p, c_int32_p, c_int32_p, c_int32_p, vp]),
@@ -179,8 +184,10 @@ def exported_symbols():
 class Handle:
     """RAII wrapper of aiy_handle (one per process and device)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int | None = 0):
         self.lib = load()
+        if device is None:
+            device = torch.cuda.current_device()
         self.device = device
         h = vp()
         rc = self.lib.aiy_create(int(device), ctypes.byref(h))

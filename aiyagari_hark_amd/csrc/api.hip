@@ -48,6 +48,9 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->h_K) (void)hipHostFree(h->h_K);
   if (h->h_hlast) (void)hipHostFree(h->h_hlast);
   if (h->hand_ev) (void)hipEventDestroy(h->hand_ev);
+  if (h->d_ge) (void)hipFree(h->d_ge);
+  for (hipEvent_t e : h->ge_ev)
+    if (e) (void)hipEventDestroy(e);
   if (h->d_hc) (void)hipFree(h->d_hc);
   if (h->d_hcd) (void)hipFree(h->d_hcd);
   for (hipEvent_t e : h->hc_ev)

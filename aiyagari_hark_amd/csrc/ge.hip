@@ -12,6 +12,7 @@
 // scipy.optimize.brentq algorithm; aiyagari_hark_amd/stationary.py _Brent is the same
 // coroutine in Python).
 #include "common.h"
+#include "ge_search.h"
 #include "internal.h"
 
 #include <algorithm>
@@ -27,79 +28,6 @@ namespace aiy {
 #define AIY_GE_EGM_CHUNK 32
 #endif
 constexpr int kGeEgmChunk = AIY_GE_EGM_CHUNK;
-// tolerances of the loose-bracketing evaluations (aiy_ge_options.loose_bracket)
-#ifndef AIY_GE_LOOSE_EGM
-#define AIY_GE_LOOSE_EGM 1e-6
-#endif
-#ifndef AIY_GE_LOOSE_HIST
-#define AIY_GE_LOOSE_HIST 1e-10
-#endif
-
-// one calibration's root search (bisect-to-a-sign-change, then brentq)
-struct RootSearch {
-  double lo, hi, xtol;
-  bool have_lo = false, have_hi = false, brent = false, done = false;
-  double flo = 0, fhi = 0, x = 0;
-  double xpre = 0, fpre = 0, xcur = 0, fcur = 0, xblk = 0, fblk = 0, spre = 0, scur = 0;
-  double xprev_eval = 0, fprev_eval = 0;
-  int method = 1;
-
-  void init(double l, double h, double tol, int meth) {
-    lo = l; hi = h; xtol = tol; method = meth;
-    x = 0.5 * (lo + hi);
-    done = !(hi - lo > xtol);
-  }
-  void update(double f) {
-    if (done) return;
-    if (method == 0) {   // oracle ge_bisect: Ks > Kd -> hi = mid
-      if (f > 0) hi = x; else lo = x;
-      if (!(hi - lo > xtol)) { done = true; x = 0.5 * (lo + hi); return; }
-      x = 0.5 * (lo + hi);
-      return;
-    }
-    if (!brent) {
-      if (f > 0) { hi = x; fhi = f; have_hi = true; } else { lo = x; flo = f; have_lo = true; }
-      if (hi - lo <= xtol) { done = true; x = 0.5 * (lo + hi); return; }
-      if (!have_lo || !have_hi) { x = 0.5 * (lo + hi); return; }
-      brent = true;
-      xpre = lo; fpre = flo; xcur = hi; fcur = fhi;
-      xblk = fblk = spre = scur = 0.0;
-      step();
-      return;
-    }
-    xpre = xprev_eval; fpre = fprev_eval; fcur = f;
-    step();
-  }
-  void step() {
-    if (fpre * fcur < 0) { xblk = xpre; fblk = fpre; spre = scur = xcur - xpre; }
-    if (std::fabs(fblk) < std::fabs(fcur)) {
-      const double xp = xcur, xc = xblk, fp = fcur, fc = fblk;
-      xpre = xp; xcur = xc; xblk = xp;
-      fpre = fp; fcur = fc; fblk = fp;
-    }
-    const double delta = 0.5 * (xtol + 4 * DBL_EPSILON * std::fabs(xcur));
-    const double sbis = 0.5 * (xblk - xcur);
-    if (fcur == 0 || std::fabs(sbis) < delta) { done = true; x = xcur; return; }
-    if (std::fabs(spre) > delta && std::fabs(fcur) < std::fabs(fpre)) {
-      double stry;
-      if (xpre == xblk) {
-        stry = -fcur * (xcur - xpre) / (fcur - fpre);
-      } else {
-        const double dpre = (fpre - fcur) / (xpre - xcur);
-        const double dblk = (fblk - fcur) / (xblk - xcur);
-        stry = -fcur * (fblk * dblk - fpre * dpre) / (dblk * dpre * (fblk - fpre));
-      }
-      if (2 * std::fabs(stry) < std::min(std::fabs(spre), 3 * std::fabs(sbis) - delta)) { spre = scur; scur = stry; }
-      else { spre = sbis; scur = sbis; }
-    } else {
-      spre = sbis; scur = sbis;
-    }
-    xprev_eval = xcur; fprev_eval = fcur;
-    xcur += std::fabs(scur) > delta ? scur : (sbis > 0 ? delta : -delta);
-    x = xcur;
-  }
-};
-
 __global__ void fill_prices_kernel(int n_cal, int S, const double* __restrict__ R, const double* __restrict__ w,
                                    double* __restrict__ Rn, double* __restrict__ Wn, double* __restrict__ Mn) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -173,6 +101,12 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   AIY_HIP(h, hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
   AIY_USE_STREAM(h, st);
+  {   // the whole search in one device-resident launch where the shape allows (ge_resident.hip)
+    const int32_t rr = ge_stationary_resident(h, M, o, r_out, K_out, Ks_out, steps_out, egm_cycles_out,
+                                              hist_iters_out, o->status_out, st);
+    if (rr < 0) return rr;
+    if (rr == 1) return AIY_OK;
+  }
   const GeLayout L = ge_layout(n_cal, S, n_a);
   char* base = static_cast<char*>(work);
   double* Rn = reinterpret_cast<double*>(base + L.Rn);
@@ -205,10 +139,12 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   std::vector<char> loose(n_cal, 0), refine(n_cal, 0);
   const bool loose_on = o->loose_bracket && o->method == 1;
   const double kLooseEgm = std::max(o->egm_tol, AIY_GE_LOOSE_EGM), kLooseHist = std::max(o->hist_tol, AIY_GE_LOOSE_HIST);
-  const double kSignMargin = 0.05;   // |K_s - K_d| / K_d that a loose evaluation's sign needs
   const unsigned sec_blocks = 1024;
   AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
 
+  std::vector<int32_t> status(n_cal, 0);   // aiy_ge_options.status_out bits
+  const int max_cyc = o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000;
+  const int max_hist = o->max_hist_iter > 0 ? o->max_hist_iter : 200000;
   std::vector<RootSearch> rs(n_cal);
   for (int c = 0; c < n_cal; ++c) {
     const double lo0 = o->r_lo ? o->r_lo[c] : -0.5 * M->delta[c];
@@ -274,7 +210,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     const double* init_m = secant ? im : pm;
     const double* init_c = secant ? ic : pc;
     h->egm_extrap = o->egm_extrapolate != 0;
-    rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000, kGeEgmChunk,
+    rc = aiy_egm_solve_impl(h, &dims, &in, o->egm_tol, max_cyc, kGeEgmChunk,
                             warm_egm ? init_m : nullptr, warm_egm ? init_c : nullptr, wm, wc2, tm, tc, cyc.data(),
                             dist.data(), stream);
     h->egm_extrap = 0;
@@ -304,8 +240,8 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     }
     h->hist_accel = o->accel > 0 ? o->accel : 0;   // accel < 0: BiCGSTAB (AIY_OPT_HIST_KRYLOV)
     h->hist_krylov = o->accel < 0;
-    rc = aiy_hist_solve(h, n_cal, S, n_a, lo, wlo, M->P, M->a_grid, o->hist_tol,
-                        o->max_hist_iter > 0 ? o->max_hist_iter : 200000, 64, mass, hw, Ks.data(), its.data(), stream);
+    rc = aiy_hist_solve(h, n_cal, S, n_a, lo, wlo, M->P, M->a_grid, o->hist_tol, max_hist, 64, mass, hw, Ks.data(),
+                        its.data(), stream);
     h->hist_accel = saved_accel;
     h->hist_krylov = saved_krylov;
     h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
@@ -313,10 +249,14 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     for (int c = 0; c < n_cal; ++c) {
       cyc_sum += cyc[c];
       it_sum += its[c];
+      // an evaluation that stopped at an iteration cap still moves the bracket by its sign;
+      // the caller learns of it through status_out
+      if (!rs[c].done && cyc[c] > max_cyc && !(dist[c] <= etol[c])) status[c] |= 1;
+      if (!rs[c].done && its[c] >= max_hist) status[c] |= 2;
       r_prev[c] = r_cur[c];
       r_cur[c] = rs[c].x;
       const double f = Ks[c] - Kd[c];
-      refine[c] = loose[c] && !(std::fabs(f) >= kSignMargin * Kd[c]);   // NaN: refine
+      refine[c] = loose[c] && !(std::fabs(f) >= kGeSignMargin * Kd[c]);   // NaN: refine
       if (!refine[c]) rs[c].update(f);
     }
     ++steps;
@@ -331,6 +271,10 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     K_out[c] = std::pow(a / (r + d), 1.0 / (1.0 - a));
     if (Ks_out) Ks_out[c] = Ks[c];
   }
+  for (int c = 0; c < n_cal; ++c)
+    if (!rs[c].done) status[c] |= 4;
+  if (o->status_out)
+    for (int c = 0; c < n_cal; ++c) o->status_out[c] = status[c];
   if (steps_out) *steps_out = steps;
   if (egm_cycles_out) *egm_cycles_out = (int32_t)std::min<long long>(cyc_sum, 0x7fffffff);
   if (hist_iters_out) *hist_iters_out = (int32_t)std::min<long long>(it_sum, 0x7fffffff);

@@ -1,0 +1,885 @@
+// Device-resident general equilibrium of the stationary Aiyagari household (build-defined
+// row E1): the WHOLE root search of every calibration in ONE launch.
+//
+// aiy_ge_stationary's host loop (ge.hip) steps all calibrations of a batch together: each
+// K_s(r) evaluation is an EGM solve (host checks every 32 cycles), a lottery launch and one
+// distribution-solve launch, and every launch lasts as long as its slowest calibration.
+// Here each calibration owns a CLUSTER of G workgroups (512 threads, one per CU; the same
+// clusters as the resident histogram, hist_resident.hip) that runs, with no host round
+// trip and no waiting for other calibrations:
+//
+//   loop over K_s(r) evaluations (the RootSearch of ge_search.h, every workgroup of the
+//   cluster on bit-identical inputs):
+//     prices      R = 1 + r, w = (1 - alpha) (alpha / (r + delta))^(alpha / (1 - alpha))
+//     start       secant start of the household tables and the mass from the last two
+//                 evaluations (x0 = cur + theta (cur - prev)), as ge.hip
+//     EGM         cycles of solve_Aiyagari (Aiyagari_Support.py:1478-1504) over the
+//                 workgroup's own asset nodes: V[s'][i] = R c_{s'}(R a_i + w l_{s'})^-rho by
+//                 the wavefront-cooperative window interpolation of egm.hip (rows another
+//                 workgroup wrote: `sc1` loads), E = beta sum_s' V P in NumPy's pairwise
+//                 order, c = E^(-1/rho), m = a + c written write-through (`sc1`); the HARK
+//                 stopping rule (sup-norm of the tables <= tol, NaN stops) rides on the
+//                 cycle's cluster barrier; the geometric extrapolation of ge.hip every 32
+//                 cycles
+//     lottery     (s, j) -> a' = m - c_s(m), m = R a_j + w l_s, bracket in the asset grid
+//     histogram   BiCGSTAB on (I - T) mass = 0 (hist_bicg.h, the kernel of hist_krylov.hip)
+//     K_s         sum mass a (cluster reduction); f = K_s - K_d; loose-bracketing sign test
+//   until the search is done; workgroup 0 writes r, K, K_s, the counts and the status.
+//
+// The launch ends when the slowest calibration's whole search ends (the host loop's launches
+// each waited for the slowest calibration of that step).  Workgroup placement: block b runs
+// on XCD b % 8 (observed dispatch, speed only), so the blocks are dealt XCD-contiguous and a
+// cluster's exchanges mostly stay inside one XCD's L2; correctness never depends on it
+// (every cross-workgroup value is written and read at agent scope).
+#include "common.h"
+#include "egm_common.h"
+#include "ge_search.h"
+#include "hist_bicg.h"
+#include "hist_cluster.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace aiy {
+
+constexpr int kGeTH = 512;
+constexpr int kGeWaves = kGeTH / kWave;   // 8
+constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
+constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
+constexpr int kGeExtrap = 32;             // cycles between extrapolation checks (ge.hip's host chunk)
+constexpr size_t kGeEgmLds = (size_t)kGeWaves * (8 * kTile + 4 * kWin) * sizeof(double);   // V tiles + windows
+
+struct GeCalDev {
+  double alpha, delta, disc, r_lo, r_hi;
+};
+
+struct GeRun {
+  int n_cal, S, n_a, G, nj, cap, n_work;
+  const double* a_grid;   // [n_cal][n_a]
+  const double* P;        // [n_cal][S][S]
+  const double* lab;      // [n_cal][S]
+  const double* beta;     // [n_cal]
+  const double* crra;     // [n_cal]
+  const GeCalDev* cal;    // [n_cal]
+  int method;
+  double r_tol, egm_tol, hist_tol;
+  int max_steps, max_cyc, max_hist;
+  int warm_hist, warm_egm, secant, loose, extrap;
+  double* tab;            // [n_cal][kGeBufs][2][S][n_a + 1]
+  double* mass;           // [n_cal][S][n_a]
+  double* pmass;          // [n_cal][S][n_a] previous evaluation's mass
+  double* pg;             // [n_cal][S][n_a] BiCGSTAB p rows
+  int* lo;                // [n_cal][S][n_a]
+  double* wlo;            // [n_cal][S][n_a]
+  double* slab;           // [n_cal][G][2][cap]
+  int* span;              // [n_cal][G][SMAX][4]
+  unsigned* ctr;          // [n_cal][kHcCtrStride]
+  unsigned long long* gran;   // [n_cal][2][G][kHcRedRec]
+  unsigned* err;
+  double* out_r;
+  double* out_K;
+  double* out_Ks;
+  int* out_steps;
+  int* out_cyc;
+  int* out_its;
+  int* out_status;
+};
+
+// Search state of one calibration, one copy per workgroup (thread 0 writes, all read).
+struct GeState {
+  RootSearch rs;
+  double R, wage, Kd, etol, htol, theta, r_cur, r_prev, Ks, dist, lam_prev, fext;
+  int steps, loose, refine, warm_egm, secant, fresh_mass, status, n, stop, nan_stop, moved, extrap;
+  int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
+  long long cyc_sum, its_sum;
+  unsigned nc_prev[2];
+  unsigned nbc;            // counting barriers passed
+};
+
+// Cluster-wide reduction of nv per-thread values (bit v of kmax: NaN-propagating max, else
+// sum) in a fixed order at every level, through tagged 8-byte granules (hist_bicg.h's
+// protocol; every workgroup computes the same s_res).  It is also a barrier: every
+// workgroup has published after all its waves drained their stores.
+template <int TH>
+__device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w, unsigned& ne, const double* vals,
+                                          int nv, unsigned kmax, double (*s_part)[TH / kWave], double* s_res,
+                                          int* s_flag, unsigned* err) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int v = 0; v < nv; ++v) {
+    const double x = (kmax >> v) & 1u ? wave_nan_max(vals[v]) : wave_sum_lane63(vals[v]);
+    if (lane == kWave - 1) s_part[v][wid] = x;
+  }
+  __syncthreads();
+  ++ne;
+  const unsigned long long tag = (unsigned long long)ne << 32;
+  unsigned long long* slot = gran + (size_t)(ne & 1) * G * kHcRedRec;
+  if (tid < nv) {
+    const int v = tid;
+    double x = s_part[v][0];
+    for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    unsigned long long* g = slot + (size_t)w * kHcRedRec + 2 * v;
+    __hip_atomic_store(g, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wid == 0) {
+    double xa[kHkRed], xb[kHkRed];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok;
+    do {
+      ok = true;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int w2 = lane + u * kWave;
+#pragma unroll
+        for (int v = 0; v < kHkRed; ++v) {
+          double x = 0.0;
+          if (v < nv && w2 < G) {
+            const unsigned long long* g = slot + (size_t)w2 * kHcRedRec + 2 * v;
+            const unsigned long long hi = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long lo = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
+            x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+          }
+          if (u == 0) xa[v] = x;
+          else xb[v] = x;
+        }
+      }
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    } while (true);
+    if (lane == 0) *s_flag = ok ? 1 : 0;
+#pragma unroll
+    for (int v = 0; v < kHkRed; ++v) {
+      if (v < nv) {
+        const bool mx = (kmax >> v) & 1u;
+        const double y = mx ? wave_nan_max(nan_max(xa[v], xb[v])) : wave_sum_lane63(xa[v] + xb[v]);
+        if (lane == kWave - 1) s_res[v] = y;
+      }
+    }
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// Interpolation pass over the workgroup's own asset columns, one 64-column tile per wave at
+// a time (wave wv: tiles wv, wv + 8; column j = j0 + 64 tile + lane = j0 + tid + 512 k, the
+// hist_bicg.h column of the same thread): for every row s of `src` (S rows of n_a + 1
+// nodes) the HARK LinearInterp at q = R a_j + Wl[s], by the window search of egm.hip over
+// agent-scope loads; sink(tile, lane column, s, q, value) takes the result.
+template <int SMAX, typename Sink>
+__device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, const double* __restrict__ a_grid,
+                                             const double* __restrict__ src_m, const double* __restrict__ src_c,
+                                             double R, const double* s_Wl, int* s_hint, double* lds_win,
+                                             Sink&& sink) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int n = n_a, n1 = n_a + 1;
+  const int ntile = (j1 - j0 + kTile - 1) / kTile;
+  double* X = lds_win + (size_t)wv * 4 * kWin;
+  double* Y = X + kWin;
+  double* XB = X + 2 * kWin;
+  double* YB = X + 3 * kWin;
+#pragma unroll 1
+  for (int tile = wv; tile < ntile; tile += kGeWaves) {
+    const int jr = j0 + tile * kTile + lane;
+    const int j = jr < j1 ? jr : j1 - 1;   // lanes past the range repeat the last column
+    const double a = a_grid[j];
+    int* hint = s_hint + tile * SMAX;
+    auto fetch = [&](int r, RowWin& wn) {
+      const int rr = r < S ? r : S - 1;
+      load_win<true>(src_m + (size_t)rr * n1, src_c + (size_t)rr * n1, n, win_base(hint[rr], n1), lane, wn);
+    };
+    unsigned redo = 0u;
+    auto step_unit = [&](int u, const RowWin& wa, const RowWin& wb) {
+      const int ra = 2 * u, rb = 2 * u + 1;
+      if (ra >= S) return;   // wave-uniform
+      const bool has_b = rb < S;
+      const int rbb = has_b ? rb : ra;
+      const bool na = __any(stage_win(wa, n, X, Y, lane));
+      const bool nb = __any(stage_win(wb, n, XB, YB, lane));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double qa = R * a + s_Wl[ra];   // mNextArray (AS:1024)
+      const double qb = R * a + s_Wl[rbb];
+      int lba, lbb;
+      bool oka, okb;
+      const double fa = search_win(wa.base, na, n, qa, X, Y, lba, oka);
+      const double fb = search_win(wb.base, nb, n, qb, XB, YB, lbb, okb);
+      hint[ra] = __builtin_amdgcn_readfirstlane(lba);
+      if (has_b) hint[rb] = __builtin_amdgcn_readfirstlane(lbb);
+      if (__any(!oka)) redo |= 1u << ra;
+      else sink(tile, jr, j, ra, qa, fa);
+      if (has_b) {
+        if (__any(!okb)) redo |= 1u << rb;
+        else sink(tile, jr, j, rb, qb, fb);
+      }
+    };
+    RowWin a0, b0, a1, b1;
+    fetch(0, a0);
+    fetch(1, b0);
+#pragma unroll 1
+    for (int u = 0; 2 * u < S; u += 2) {
+      fetch(2 * u + 2, a1);
+      fetch(2 * u + 3, b1);
+      step_unit(u, a0, b0);
+      fetch(2 * u + 4, a0);
+      fetch(2 * u + 5, b0);
+      step_unit(u + 1, a1, b1);
+    }
+#pragma unroll 1
+    while (redo != 0u) {   // wave-uniform
+      const int s = __builtin_ctz(redo);
+      redo &= redo - 1u;
+      const double q = R * a + s_Wl[s];
+      int lb;
+      const double f = interp_row_global_agent(src_m + (size_t)s * n1, src_c + (size_t)s * n1, n, q, lb);
+      hint[s] = __builtin_amdgcn_readfirstlane(lb);
+      sink(tile, jr, j, s, q, f);
+    }
+  }
+}
+
+// One EGM cycle of the workgroup's own nodes: src (cycle n - 1; nullptr: the terminal
+// c = m) -> dst (cycle n).  Returns the workgroup's part of the HARK distance (track).
+template <int SMAX, int SC, int PK>
+__device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, const double* __restrict__ a_grid,
+                                               const double* src_m, const double* src_c, double* dst_m,
+                                               double* dst_c, bool track, double R, double beta, double gam,
+                                               const double* s_Wl, const double* s_Pe, int* s_hint,
+                                               double* lds_v, double* lds_win) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int n1 = n_a + 1;
+  double* Vw = lds_v + (size_t)wv * SMAX * kTile;   // this wave's V[s'][lane]
+  const int ntile = (j1 - j0 + kTile - 1) / kTile;
+  double dmax = 0.0;
+  if (src_m == nullptr) {   // terminal guess: IdentityFunction (AS:898) of mNextArray
+#pragma unroll 1
+    for (int tile = wv; tile < ntile; tile += kGeWaves) {
+      const int jr = j0 + tile * kTile + lane;
+      const int j = jr < j1 ? jr : j1 - 1;
+      const double a = a_grid[j];
+      for (int sp = 0; sp < S; ++sp) {
+        const double c = (R * a + s_Wl[sp]) * 1.0;
+        Vw[sp * kTile + lane] = R * marg_u<PK>(c, gam);   // read back by the same lane only
+      }
+      for (int s = 0; s < S; ++s) {
+        double sum;
+        if constexpr (SC > 0) sum = pairwise_dot<SC>(Vw + lane, s_Pe + s * SC);
+        else sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vw[t * kTile + lane] * uniform_f64(s_Pe[s * S + t]); });
+        const double c = inv_marg<PK>(beta * sum, gam);
+        store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], a + c);
+        store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
+        if (j == 0) {
+          store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
+          store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
+        }
+      }
+    }
+    return 0.0;
+  }
+  // tiles one after another per wave: V of a tile's rows (phase 1), then its outputs
+  int cur_tile = -1;
+  auto flush = [&](int tile) {   // phase 2 of `tile` (its V complete; each lane reads its own)
+    const int jr = j0 + tile * kTile + lane;
+    const int j = jr < j1 ? jr : j1 - 1;
+    const double a = a_grid[j];
+    for (int s = 0; s < S; ++s) {
+      double pm = 0.0, pc = 0.0;
+      if (track) {
+        pm = load_f64_agent(&src_m[(size_t)s * n1 + j + 1]);
+        pc = load_f64_agent(&src_c[(size_t)s * n1 + j + 1]);
+      }
+      double sum;
+      if constexpr (SC > 0) sum = pairwise_dot<SC>(Vw + lane, s_Pe + s * SC);
+      else sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vw[t * kTile + lane] * uniform_f64(s_Pe[s * S + t]); });
+      const double E = beta * sum;                     // EndOfPrdvP (AS:1485)
+      const double c = inv_marg<PK>(E, gam);           // AS:1490
+      const double m = a + c;                          // AS:1499
+      store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], m);
+      store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
+      if (track) dmax = nan_max(dmax, nan_max(fabs(m - pm), fabs(c - pc)));
+      if (j == 0) {   // the (1e-7, 1e-7) node (AS:1503-1504)
+        store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
+        store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
+      }
+    }
+  };
+  // the window pass visits a tile's rows in order, the redo rows after them: the tile's V
+  // is complete when the pass moves to the next tile (or ends)
+  ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, src_m, src_c, R, s_Wl, s_hint, lds_win,
+                     [&](int tile, int, int, int sp, double, double f) {
+                       if (tile != cur_tile) {
+                         if (cur_tile >= 0) flush(cur_tile);
+                         cur_tile = tile;
+                       }
+                       Vw[sp * kTile + lane] = R * marg_u<PK>(f, gam);   // RnextArray * MargValueFuncCRRA
+                     });
+  if (cur_tile >= 0) flush(cur_tile);
+  return dmax;
+}
+
+template <int SMAX, int SC, int KC>
+__global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
+  constexpr int TH = kGeTH;
+  extern __shared__ double dyn[];   // histogram: span buffer + v; EGM: V tiles + windows (aliased)
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  __shared__ double s_Pe[SMAX * SMAX];   // P[s][s'] unpadded (egm_phase2's layout)
+  __shared__ double s_Wl[SMAX];          // w l(s')
+  __shared__ int s_hint[kGeMaxTiles * SMAX];
+  __shared__ unsigned s_nc;
+  __shared__ GeState st;
+
+  const int per = gridDim.x >> 3;
+  const int u = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-contiguous work order
+  if (u >= g.n_work) return;
+  const int G = g.G, S = g.S, n_a = g.n_a, n1 = n_a + 1;
+  const int cal = u / G, w = u - cal * G;
+  const int tid = threadIdx.x;
+  const int j0 = w * g.nj, j1 = min(j0 + g.nj, n_a);
+  const double* a_grid = g.a_grid + (size_t)cal * n_a;
+  const double beta = g.beta[cal], gam = g.crra[cal];
+  const GeCalDev cd = g.cal[cal];
+  const size_t tab_sz = (size_t)S * n1;
+  double* tab = g.tab + (size_t)cal * kGeBufs * 2 * tab_sz;
+  auto tabm = [&](int b) { return tab + (size_t)b * 2 * tab_sz; };
+  auto tabc = [&](int b) { return tab + (size_t)b * 2 * tab_sz + tab_sz; };
+  const size_t row0 = (size_t)cal * S * n_a;
+  double* X = g.mass + row0;
+  double* PX = g.pmass + row0;
+  int* LO = g.lo + row0;
+  double* WL = g.wlo + row0;
+  unsigned* ctr = g.ctr + (size_t)cal * kHcCtrStride;
+  unsigned long long* cw = reinterpret_cast<unsigned long long*>(ctr + 2);   // counting-barrier words
+  unsigned long long* gran = g.gran + (size_t)cal * 2 * G * kHcRedRec;
+  unsigned nb = 0, ne = 0;   // plain barriers / reductions passed (hk_solve counts on)
+  const int pk = gam == 1.0 ? 1 : (gam == 3.0 ? 3 : (gam == 5.0 ? 5 : 0));
+
+  const HkShared<SMAX, KC, TH> L{dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop};
+  double* lds_v = dyn;
+  double* lds_win = dyn + (size_t)kGeWaves * SMAX * kTile;
+
+  for (int q = tid; q < S * S; q += TH) s_Pe[q] = g.P[(size_t)cal * S * S + q];
+  for (int q = tid; q < kGeMaxTiles * SMAX; q += TH) s_hint[q] = -1;
+  if (tid == 0) {
+    st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method);
+    st.r_cur = st.r_prev = 0.0;
+    st.Ks = 0.0;
+    st.steps = 0;
+    st.refine = 0;
+    st.status = 0;
+    st.cyc_sum = st.its_sum = 0;
+    st.nc_prev[0] = st.nc_prev[1] = 0u;
+    st.nbc = 0u;
+    for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
+  }
+  __syncthreads();
+  auto plain_barrier = [&]() -> bool {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ++nb;
+    return hc_barrier(g.err, ctr, (unsigned)G * nb, &s_flag);
+  };
+
+  while (!st.rs.done && st.steps < g.max_steps) {
+    // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
+    if (tid == 0) {
+      const double r = st.rs.x, a = cd.alpha, d = cd.delta;
+      const double KtoL = pow(a / (r + d), 1.0 / (1.0 - a));
+      st.R = 1.0 + r;
+      st.wage = (1.0 - a) * pow(KtoL, a);
+      st.Kd = KtoL;
+      st.loose = g.loose && g.method == 1 && !st.rs.brent && !st.rs.done && !st.refine;
+      st.etol = st.loose ? fmax(g.egm_tol, AIY_GE_LOOSE_EGM) : g.egm_tol;
+      st.htol = st.loose ? fmax(g.hist_tol, AIY_GE_LOOSE_HIST) : g.hist_tol;
+      st.warm_egm = g.warm_egm && st.steps > 0;
+      st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
+      st.fresh_mass = !(g.warm_hist && st.steps > 0);
+      double th = 0.0;
+      if (st.secant) {
+        const double den = st.r_cur - st.r_prev;
+        th = den != 0.0 ? (r - st.r_cur) / den : 0.0;
+        th = isfinite(th) ? fmax(-1.0, fmin(1.0, th)) : 0.0;
+      }
+      st.theta = th;
+      st.extrap = g.extrap;
+      st.moved = 0;
+    }
+    __syncthreads();
+    if (tid < S) s_Wl[tid] = st.wage * g.lab[(size_t)cal * S + tid];   // W l(s') (mNextArray, AS:1024)
+    const double R = st.R, theta = st.theta;
+    // ---- starting tables: the secant start into `init` (own nodes), else cur ----
+    const bool secant = st.secant != 0, warm = st.warm_egm != 0;
+    const int b_cur = st.buf[2], b_prev = st.buf[3], b_init = st.buf[4];
+    if (secant) {
+      for (int s = 0; s < S; ++s) {
+        for (int k = j0 + tid; k < j1; k += TH) {
+          const size_t o = (size_t)s * n1 + k + 1;
+          const double cm = load_f64_agent(&tabm(b_cur)[o]), pm = load_f64_agent(&tabm(b_prev)[o]);
+          const double cc = load_f64_agent(&tabc(b_cur)[o]), pc = load_f64_agent(&tabc(b_prev)[o]);
+          store_f64_agent(&tabm(b_init)[o], theta == 0.0 ? cm : cm + theta * (cm - pm));
+          store_f64_agent(&tabc(b_init)[o], theta == 0.0 ? cc : cc + theta * (cc - pc));
+        }
+        if (j0 == 0 && tid == 0) {
+          store_f64_agent(&tabm(b_init)[(size_t)s * n1], kBorrowNode);
+          store_f64_agent(&tabc(b_init)[(size_t)s * n1], kBorrowNode);
+        }
+      }
+    }
+    // ---- the household solve ([HARK] solve_agent: cycles until the sup-norm change of the
+    //      tables is <= tol, NaN stops; cold: cycle 1 from the terminal guess) ----
+    const double* init_m = secant ? tabm(b_init) : (warm ? tabm(b_cur) : nullptr);
+    const double* init_c = secant ? tabc(b_init) : (warm ? tabc(b_cur) : nullptr);
+    int final_buf = -1;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      if (!plain_barrier()) return;   // every workgroup's start tables visible
+      const bool ext = st.extrap != 0 && attempt == 0;
+      if (tid == 0) {
+        st.lam_prev = -1.0;
+        st.moved = 0;
+        st.nan_stop = 0;
+      }
+      int n = 1;
+      const int last_allowed = g.max_cyc + 1;
+      bool converged = false;
+      while (true) {
+        const int b_dst = st.buf[n & 1], b_src = st.buf[(n - 1) & 1];
+        const double* sm = n == 1 ? init_m : tabm(b_src);
+        const double* sc = n == 1 ? init_c : tabc(b_src);
+        const bool track = n >= 2;
+        double dl;
+        if (pk == 1)
+          dl = ge_egm_cycle<SMAX, SC, 1>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
+                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+        else if (pk == 3)
+          dl = ge_egm_cycle<SMAX, SC, 3>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
+                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+        else if (pk == 5)
+          dl = ge_egm_cycle<SMAX, SC, 5>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
+                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+        else
+          dl = ge_egm_cycle<SMAX, SC, 0>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
+                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+        // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
+        // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
+        const bool want_value = ext && n >= kGeExtrap - 1 &&
+                                ((n % kGeExtrap) == kGeExtrap - 1 || (n % kGeExtrap) == 0);
+        double dclu = 0.0;
+        bool go;
+        if (want_value) {
+          double v[1] = {dl};
+          if (!ge_reduce<TH>(gran, G, w, ne, v, 1, 1u, s_part, s_res, &s_flag, g.err)) return;
+          dclu = s_res[0];
+          go = dclu > st.etol;   // NaN: stop (HARK: go = distance > tolerance)
+          if (tid == 0) st.nan_stop = dclu != dclu;
+        } else {
+          const double dw = wave_nan_max(dl);
+          if ((tid & (kWave - 1)) == 0) s_part[0][tid / kWave] = dw;
+          __syncthreads();
+          unsigned flag = 0u;
+          if (tid == 0) {
+            double d = s_part[0][0];
+            for (int q = 1; q < TH / kWave; ++q) d = nan_max(d, s_part[0][q]);
+            flag = (d > st.etol ? 1u : 0u) | (d != d ? (1u << 16) : 0u);
+            ++st.nbc;
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          const unsigned k = st.nbc, par = k & 1u;
+          if (!hc_barrier_count(g.err, &cw[par], (unsigned)G * ((k + par) / 2), flag, &s_nc, &s_flag)) return;
+          if (tid == 0) {
+            const unsigned dlt = s_nc - st.nc_prev[par];
+            st.nc_prev[par] = s_nc;
+            st.stop = (dlt & 0xffffu) == 0u || (dlt >> 16) != 0u;
+            st.nan_stop = (dlt >> 16) != 0u;
+          }
+          __syncthreads();
+          go = !st.stop;
+        }
+        if (track && !go) {
+          converged = true;
+          break;
+        }
+        if (n >= last_allowed) break;
+        // geometric extrapolation at the checks (ge.hip / egm.hip egm_extrap_kernel)
+        if (want_value && (n % kGeExtrap) == 0) {
+          if (tid == 0) {
+            const double d1 = dclu, d0 = st.dist, lam = d1 / d0;
+            st.fext = 0.0;
+            if (n >= 4 && d1 > 100.0 * st.etol && lam > 0.5 && lam < 0.999 && st.lam_prev > 0.0 &&
+                fabs(lam - st.lam_prev) < 0.2 * (1.0 - lam)) {
+              st.fext = lam / (1.0 - lam);
+              st.moved = 1;
+            }
+            st.lam_prev = lam;
+          }
+          __syncthreads();
+          const double f = st.fext;
+          if (f != 0.0) {
+            double* cm = tabm(b_dst);
+            double* cc = tabc(b_dst);
+            const double* pm = tabm(b_src);
+            const double* pc = tabc(b_src);
+            for (int s = 0; s < S; ++s)
+              for (int k = j0 + tid; k < j1; k += TH) {
+                const size_t o = (size_t)s * n1 + k + 1;
+                const double x = load_f64_agent(&cm[o]), y = load_f64_agent(&cc[o]);
+                store_f64_agent(&cm[o], x + f * (x - load_f64_agent(&pm[o])));
+                store_f64_agent(&cc[o], y + f * (y - load_f64_agent(&pc[o])));
+              }
+            if (!plain_barrier()) return;
+          }
+        } else if (want_value) {
+          if (tid == 0) st.dist = dclu;
+        }
+        ++n;
+      }
+      if (tid == 0) {
+        st.n = n;
+        if (!converged) st.status |= 1;
+      }
+      __syncthreads();
+      final_buf = st.buf[n & 1];
+      // an extrapolated solve that ended in NaN: the whole solve again, plain (ge.hip)
+      if (!(st.moved && st.nan_stop)) break;
+      if (tid == 0) {
+        st.extrap = 0;
+        st.status &= ~1;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      st.cyc_sum += st.n;
+      // buffer roles: prev <- cur, cur <- the solve's final tables, the freed ones ping-pong
+      const int fb = final_buf;
+      const int other = st.buf[0] == fb ? st.buf[1] : st.buf[0];
+      const int old_prev = st.buf[3];
+      st.buf[3] = st.buf[2];
+      st.buf[2] = fb;
+      st.buf[0] = other;
+      st.buf[1] = old_prev;
+    }
+    __syncthreads();
+    // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
+    {
+      const double* fm = tabm(st.buf[2]);
+      const double* fc = tabc(st.buf[2]);
+      const bool have_prev = st.steps > 0;
+      ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, fm, fc, R, s_Wl, s_hint, lds_win,
+                         [&](int, int jr, int, int s, double q, double c) {
+                           if (jr >= j1) return;
+                           const double ap = q - c;
+                           const size_t o = (size_t)s * n_a + jr;
+                           int d = -1;
+                           if (have_prev) {   // last evaluation's bracket as the first guess
+                             const int h = LO[o];
+                             if (h >= 0 && h < n_a - 1 && a_grid[h] <= ap && ap < a_grid[h + 1]) d = h;
+                           }
+                           if (d < 0) {       // searchsorted(a_grid, a', 'right') - 1
+                             int lo = 0, hi = n_a;
+                             while (lo < hi) {
+                               const int mid = lo + ((hi - lo) >> 1);
+                               if (a_grid[mid] <= ap) lo = mid + 1; else hi = mid;
+                             }
+                             d = lo - 1;
+                           }
+                           d = d < 0 ? 0 : (d > n_a - 2 ? n_a - 2 : d);
+                           double wl = (a_grid[d + 1] - ap) / (a_grid[d + 1] - a_grid[d]);
+                           wl = wl < 0.0 ? 0.0 : (wl > 1.0 ? 1.0 : wl);
+                           LO[o] = d;
+                           WL[o] = wl;
+                         });
+    }
+    // ---- the distribution's start (own columns) ----
+    if (st.fresh_mass) {
+      const double u0 = 1.0 / ((double)S * n_a);
+      for (int s = 0; s < S; ++s)
+        for (int k = j0 + tid; k < j1; k += TH) X[(size_t)s * n_a + k] = u0;
+    } else if (warm) {
+      for (int s = 0; s < S; ++s)
+        for (int k = j0 + tid; k < j1; k += TH) {
+          const size_t o = (size_t)s * n_a + k;
+          const double x = X[o];
+          if (secant) X[o] = theta == 0.0 ? x : x + theta * (x - PX[o]);
+          PX[o] = x;
+        }
+    }
+    __syncthreads();
+    // ---- the stationary distribution: BiCGSTAB on (I - T) mass = 0 ----
+    int mv;
+    {
+      HkArgs hk;
+      hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
+      hk.LO = LO; hk.WL = WL; hk.X = X; hk.Pg = g.pg + row0; hk.Vg = nullptr;
+      hk.slab_cl = g.slab + (size_t)cal * G * 2 * g.cap;
+      hk.span_cl = g.span + (size_t)cal * G * SMAX * 4;
+      hk.ctr = ctr; hk.gran = gran; hk.Pc = g.P + (size_t)cal * S * S;
+      hk.max_iter = g.max_hist; hk.err = g.err;
+      hk.tol = st.htol;
+      mv = hk_solve<SMAX, KC, TH>(hk, L, nb, ne);
+    }
+    if (mv < 0) return;
+    // ---- K_s = sum mass a over the cluster ----
+    double part = 0.0;
+    for (int k = j0 + tid; k < j1; k += TH) {
+      double ms = 0.0;
+      for (int s = 0; s < S; ++s) ms += X[(size_t)s * n_a + k];
+      part += ms * a_grid[k];
+    }
+    {
+      double v[1] = {part};
+      if (!ge_reduce<TH>(gran, G, w, ne, v, 1, 0u, s_part, s_res, &s_flag, g.err)) return;
+    }
+    if (tid == 0) {
+      const double Ks = s_res[0];
+      st.its_sum += mv;
+      if (mv >= g.max_hist) st.status |= 2;
+      st.r_prev = st.r_cur;
+      st.r_cur = st.rs.x;
+      const double f = Ks - st.Kd;
+      st.refine = st.loose && !(fabs(f) >= kGeSignMargin * st.Kd);   // NaN: refine
+      if (!st.refine) st.rs.update(f);
+      st.Ks = Ks;
+      ++st.steps;
+    }
+    __syncthreads();
+  }
+  if (w == 0 && tid == 0) {
+    const double r = st.rs.x, a = cd.alpha, d = cd.delta;
+    g.out_r[cal] = r;
+    g.out_K[cal] = pow(a / (r + d), 1.0 / (1.0 - a));
+    g.out_Ks[cal] = st.Ks;
+    g.out_steps[cal] = st.steps;
+    g.out_cyc[cal] = (int)min(st.cyc_sum, 0x7fffffffll);
+    g.out_its[cal] = (int)min(st.its_sum, 0x7fffffffll);
+    g.out_status[cal] = st.status | (st.rs.done ? 0 : 4);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+struct GePlan {
+  int G = 0, nj = 0, kc = 0, smax = 0, sc = 0, cap = 0, blocks = 0;
+  size_t lds = 0;
+  const void* fn = nullptr;
+};
+
+template <int SMAX, int SC, int KC>
+static const void* ge_fn() {
+  return reinterpret_cast<const void*>(ge_cluster_kernel<SMAX, SC, KC>);
+}
+
+// Launch shape of the device-resident search for (n_cal, S, n_a): every calibration's
+// cluster resident at once (n_cal G workgroups, one per CU, within the handle's CU limit).
+static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
+  if (S < 1 || S > 8 || n_a < 2 || n_cal < 1) return false;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
+  if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
+  const int th = kGeTH;
+  const int g_min = (n_a + 2 * th - 1) / (2 * th);
+  const int g_cap = h->hist_cluster_cap > 0 ? h->hist_cluster_cap : 32;
+  int G = std::max(g_min, std::min(std::min(g_cap, kHcMaxG), cus / n_cal));
+  G = std::min(G, n_a);
+  p.nj = (n_a + G - 1) / G;
+  p.G = (n_a + p.nj - 1) / p.nj;
+  if (p.nj > kGeMaxTiles * kTile) return false;
+  if ((long long)p.G * n_cal > cus) return false;
+  p.kc = p.nj <= th ? 1 : 2;
+  p.smax = 8;
+  p.sc = S == 7 ? 7 : 0;
+  if (p.sc == 7) p.fn = p.kc == 1 ? ge_fn<8, 7, 1>() : ge_fn<8, 7, 2>();
+  else p.fn = p.kc == 1 ? ge_fn<8, 0, 1>() : ge_fn<8, 0, 2>();
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
+  int lds_dev = 0;
+  if (hipDeviceGetAttribute(&lds_dev, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess)
+    return false;
+  const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
+  const size_t stat = fa.sharedSizeBytes;
+  if (stat + 4096 >= lds_total) return false;
+  p.lds = (lds_total - stat - 1024) / 256 * 256;
+  const size_t vbytes = (size_t)p.kc * p.smax * th * sizeof(double);   // BiCGSTAB v behind the spans
+  if (p.lds < kGeEgmLds || p.lds <= vbytes + 4096) return false;
+  p.cap = (int)((p.lds - vbytes) / sizeof(double));
+  p.blocks = (p.G * n_cal + 7) / 8 * 8;
+  return true;
+}
+
+struct GeScratch {
+  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, bytes;
+};
+static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
+  GeScratch L;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
+  const size_t pts = (size_t)n_cal * S * n_a;
+  L.tab = take((size_t)n_cal * kGeBufs * 2 * S * (n_a + 1) * sizeof(double));
+  L.mass = take(pts * 8); L.pmass = take(pts * 8); L.pg = take(pts * 8);
+  L.lo = take(pts * 4); L.wlo = take(pts * 8);
+  L.slab = take((size_t)n_cal * G * 2 * cap * sizeof(double));
+  L.span = take((size_t)n_cal * G * 8 * 4 * sizeof(int));
+  L.ctr = take((size_t)n_cal * kHcCtrStride * sizeof(unsigned));
+  L.gran = take((size_t)n_cal * 2 * G * kHcRedRec * sizeof(unsigned long long));
+  L.err = take(256);
+  L.cal = take((size_t)n_cal * sizeof(GeCalDev));
+  L.outd = take((size_t)n_cal * 3 * sizeof(double));
+  L.outi = take((size_t)n_cal * 4 * sizeof(int));
+  L.bytes = o;
+  return L;
+}
+
+// The whole search in one launch when the shape allows it (1: done; 0: not applicable, the
+// caller runs the host-driven loop; < 0: error).
+int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, const aiy_ge_options* o, double* r_out,
+                               double* K_out, double* Ks_out, int32_t* steps_out, int32_t* cyc_out,
+                               int32_t* its_out, int32_t* status_out, hipStream_t st) {
+  if (!h->ge_resident || o->accel >= 0) return 0;   // BiCGSTAB distribution solves only
+  const int n_cal = M->n_cal, S = M->S, n_a = M->n_a;
+  GePlan p;
+  if (!ge_make_plan(h, n_cal, S, n_a, p)) return 0;
+  if (hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, kGeTH, p.lds) != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap);
+  if (L.bytes > h->ge_cap) {
+    if (h->d_ge) (void)hipFree(h->d_ge);
+    h->d_ge = nullptr;
+    h->ge_cap = 0;
+    AIY_HIP(h, hipMalloc(&h->d_ge, L.bytes));
+    h->ge_cap = L.bytes;
+  }
+  char* base = static_cast<char*>(h->d_ge);
+  std::vector<GeCalDev> cals(n_cal);
+  for (int c = 0; c < n_cal; ++c) {
+    cals[c].alpha = M->alpha[c];
+    cals[c].delta = M->delta[c];
+    cals[c].disc = M->disc[c];
+    cals[c].r_lo = o->r_lo ? o->r_lo[c] : -0.5 * M->delta[c];
+    cals[c].r_hi = o->r_hi ? o->r_hi[c] : 1.0 / M->disc[c] - 1.0 - 1e-9;
+  }
+  GeRun g;
+  g.n_cal = n_cal; g.S = S; g.n_a = n_a; g.G = p.G; g.nj = p.nj; g.cap = p.cap; g.n_work = n_cal * p.G;
+  g.a_grid = M->a_grid; g.P = M->P; g.lab = M->lab; g.beta = M->beta; g.crra = M->crra;
+  g.cal = reinterpret_cast<const GeCalDev*>(base + L.cal);
+  g.method = o->method; g.r_tol = o->r_tol; g.egm_tol = o->egm_tol; g.hist_tol = o->hist_tol;
+  g.max_steps = o->max_steps;
+  g.max_cyc = o->max_egm_cycles > 0 ? o->max_egm_cycles : 5000;
+  g.max_hist = o->max_hist_iter > 0 ? o->max_hist_iter : 200000;
+  g.warm_hist = o->warm_hist != 0; g.warm_egm = o->warm_egm != 0;
+  g.secant = o->secant_start != 0; g.loose = o->loose_bracket != 0; g.extrap = o->egm_extrapolate != 0;
+  g.tab = reinterpret_cast<double*>(base + L.tab);
+  g.mass = reinterpret_cast<double*>(base + L.mass);
+  g.pmass = reinterpret_cast<double*>(base + L.pmass);
+  g.pg = reinterpret_cast<double*>(base + L.pg);
+  g.lo = reinterpret_cast<int*>(base + L.lo);
+  g.wlo = reinterpret_cast<double*>(base + L.wlo);
+  g.slab = reinterpret_cast<double*>(base + L.slab);
+  g.span = reinterpret_cast<int*>(base + L.span);
+  g.ctr = reinterpret_cast<unsigned*>(base + L.ctr);
+  g.gran = reinterpret_cast<unsigned long long*>(base + L.gran);
+  g.err = reinterpret_cast<unsigned*>(base + L.err);
+  double* outd = reinterpret_cast<double*>(base + L.outd);
+  int* outi = reinterpret_cast<int*>(base + L.outi);
+  g.out_r = outd; g.out_K = outd + n_cal; g.out_Ks = outd + 2 * n_cal;
+  g.out_steps = outi; g.out_cyc = outi + n_cal; g.out_its = outi + 2 * n_cal; g.out_status = outi + 3 * n_cal;
+  AIY_HIP(h, hipMemcpyAsync(base + L.cal, cals.data(), sizeof(GeCalDev) * n_cal, hipMemcpyHostToDevice, st));
+  AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n_cal * kHcCtrStride * sizeof(unsigned), st));
+  AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n_cal * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
+  AIY_HIP(h, hipMemsetAsync(g.err, 0, 256, st));
+  for (hipEvent_t& e : h->ge_ev)
+    if (!e) AIY_HIP(h, hipEventCreate(&e));
+  void* args[] = {&g};
+  AIY_HIP(h, hipEventRecord(h->ge_ev[0], st));
+  AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(kGeTH), args, p.lds, st));
+  AIY_HIP(h, hipEventRecord(h->ge_ev[1], st));
+  std::vector<double> hd(3 * (size_t)n_cal);
+  std::vector<int> hi(4 * (size_t)n_cal);
+  unsigned err = 0;
+  AIY_HIP(h, hipMemcpyAsync(&err, g.err, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  AIY_HIP(h, hipMemcpyAsync(hd.data(), outd, sizeof(double) * 3 * n_cal, hipMemcpyDeviceToHost, st));
+  AIY_HIP(h, hipMemcpyAsync(hi.data(), outi, sizeof(int) * 4 * n_cal, hipMemcpyDeviceToHost, st));
+  AIY_HIP(h, hipStreamSynchronize(st));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, h->ge_ev[0], h->ge_ev[1]) == hipSuccess) {
+    h->ge_ms_sum += ms;
+    h->ge_launches += 1;
+  }
+  if (err == 1u) return fail(h, AIY_ERR_STATE, "device-resident GE: cluster barrier timed out (workgroups not co-resident?)");
+  if (err) return fail(h, AIY_ERR_STATE, "device-resident GE: histogram shape does not fit (error %u)", err);
+  long long cyc = 0, its = 0;
+  int steps = 0;
+  for (int c = 0; c < n_cal; ++c) {
+    r_out[c] = hd[c];
+    K_out[c] = hd[n_cal + c];
+    if (Ks_out) Ks_out[c] = hd[2 * n_cal + c];
+    steps = std::max(steps, hi[c]);
+    cyc += hi[n_cal + c];
+    its += hi[2 * n_cal + c];
+    if (status_out) status_out[c] = hi[3 * n_cal + c];
+    h->ge_points += (double)hi[2 * n_cal + c] * S * n_a;
+    h->ge_egm_cycles += hi[n_cal + c];
+  }
+  if (steps_out) *steps_out = steps;
+  if (cyc_out) *cyc_out = (int32_t)std::min<long long>(cyc, 0x7fffffff);
+  if (its_out) *its_out = (int32_t)std::min<long long>(its, 0x7fffffff);
+  return 1;
+}
+
+}  // namespace aiy
+
+using namespace aiy;
+
+extern "C" int32_t aiy_ge_resident_plan(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, int32_t* out4) {
+  if (!h || !out4) return AIY_ERR_ARG;
+  GePlan p;
+  if (!h->ge_resident || !ge_make_plan(h, n_cal, S, n_a, p)) {
+    out4[0] = out4[1] = out4[2] = out4[3] = 0;
+    return 0;
+  }
+  out4[0] = p.G;
+  out4[1] = p.nj;
+  out4[2] = p.kc;
+  out4[3] = p.blocks;
+  return 1;
+}
+
+extern "C" int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, double* point_matvecs,
+                                       double* egm_cycles, int32_t reset) {
+  if (!h) return AIY_ERR_ARG;
+  if (ms_sum) *ms_sum = h->ge_ms_sum;
+  if (launches) *launches = h->ge_launches;
+  if (point_matvecs) *point_matvecs = h->ge_points;
+  if (egm_cycles) *egm_cycles = h->ge_egm_cycles;
+  if (reset) {
+    h->ge_ms_sum = 0.0;
+    h->ge_launches = 0;
+    h->ge_points = 0.0;
+    h->ge_egm_cycles = 0.0;
+  }
+  return AIY_OK;
+}

@@ -1,0 +1,695 @@
+// The BiCGSTAB distribution solve of one calibration's cluster (build-defined row E2,
+// Krylov mode) as a device function: hist_krylov.hip runs one solve per launch,
+// ge_resident.hip many solves per launch inside its device-resident GE search.
+// See hist_krylov.hip for the algorithm.
+#pragma once
+
+#include "common.h"
+#include "hist_cluster.h"
+
+namespace aiy {
+
+constexpr int kHkRed = 8;   // partial sums per reduction (at most)
+constexpr int kHkStall = 256;   // matvecs without a 10 % residual gain that count as a stall
+static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
+
+// shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
+__device__ __forceinline__ double hk_rhat(unsigned q) {
+  unsigned h = q * 0x9E3779B1u + 0x7F4A7C15u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (double)(int)h * (1.0 / 2147483648.0);
+}
+
+// Phase timing (diagnostic builds, -DAIY_DIAG_PHASES=<block>: that block and the next 9,
+// i.e. one calibration's cluster at Table II size): time since the previous
+// mark is added to slot k: 0 push, 1 publish, 2 matvec barrier, 3 gather + mix,
+// 4 reductions (partials, publish, barrier, read), 5 vector updates
+#ifdef AIY_DIAG_PHASES
+#define HK_PH(k)                                                        \
+  do {                                                                  \
+    if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10) { \
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();   \
+      if ((k) >= 0) ph[(k)] += tn - tq;                                 \
+      tq = tn;                                                          \
+    }                                                                   \
+  } while (0)
+#else
+#define HK_PH(k) \
+  do {           \
+  } while (0)
+#endif
+
+template <int SMAX, int KC, int TH>
+struct HkShared {
+  double* Tacc;                    // span buffer (cap doubles); for SMAX <= 8 then v
+  int* s_base;                     // [SMAX]
+  int (*s_pub)[2];                 // [2 SMAX][2]
+  int* s_tot;
+  HcCand (*s_cand)[kHcCand];       // [SMAX][kHcCand]
+  int* s_ncand;                    // [SMAX]
+  unsigned short* s_cinfo;         // [KC SMAX TH]
+  double* s_P;                     // [SMAX SMAX]
+  double (*s_part)[TH / kWave];    // [kHkRed]
+  double* s_res;                   // [kHkRed]
+  int* s_flag;
+  int* s_stop;
+};
+
+// One calibration's BiCGSTAB distribution solve by the workgroups of its cluster (this
+// workgroup: w of G, own columns [j0, j1)); shared by hist_bicg_kernel (one solve per
+// launch) and the device-resident GE search (ge_resident.hip, many solves per launch).
+struct HkArgs {
+  int G, S, n_a, cap, w, j0, j1;
+  const int* LO;          // [S][n_a] lottery of the calibration (index)
+  const double* WL;       // [S][n_a] lottery weight on lo
+  double* X;              // [S][n_a] in: start, out: T x (own columns)
+  double* Pg;             // [S][n_a] p scratch rows
+  double* Vg;             // v block of this workgroup in HBM (SMAX > 8)
+  double* slab_cl;        // [G][2][cap]
+  int* span_cl;           // [G][SMAX][4]
+  unsigned* ctr;          // cluster barrier counter
+  unsigned long long* gran;   // [2][G][kHcRedRec] reduction granules
+  const double* Pc;       // [S][S]
+  double tol;
+  int max_iter;
+  unsigned* err;
+};
+
+// Returns the matvecs of the solve, or -1 when the cluster stops (error word set: a
+// timeout, a span that does not fit, too many covering workgroups).  nb / ne: the
+// cluster barriers / reductions passed so far in this launch (counted on).
+template <int SMAX, int KC, int TH>
+__device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
+                                        unsigned& ne) {
+  constexpr bool kVlds = SMAX <= 8;
+#ifdef AIY_DIAG_PHASES
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tq = 0;
+#endif
+  double* Tacc = L.Tacc;
+  int* s_base = L.s_base;
+  int (*s_pub)[2] = L.s_pub;
+  HcCand (*s_cand)[kHcCand] = L.s_cand;
+  int* s_ncand = L.s_ncand;
+  unsigned short* s_cinfo = L.s_cinfo;
+  double* s_P = L.s_P;
+  double (*s_part)[TH / kWave] = L.s_part;
+  double* s_res = L.s_res;
+  int& s_flag = *L.s_flag;
+  int& s_stop = *L.s_stop;
+  int& s_tot = *L.s_tot;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
+  const int G = r.G, S = r.S, n_a = r.n_a, cap = r.cap;
+  const int w = r.w;
+  const int j0 = r.j0;
+  const int j1 = r.j1;
+  unsigned* ctr = r.ctr;
+  unsigned long long* gran = r.gran;
+  const int* LO = r.LO;
+  const double* WL = r.WL;
+  double* X = r.X;   // x: the iterate, own columns read-modify-written
+  double* slab_cl = r.slab_cl;
+  const double* __restrict__ Pc = r.Pc;
+  int* span_cl = r.span_cl;
+
+  // ---- setup (as hist_cluster_kernel): P, own spans, covering candidates ----
+  for (int q = tid; q < SMAX * SMAX; q += TH) {
+    const int s = q / SMAX, sp = q - s * SMAX;
+    s_P[q] = (s < S && sp < S) ? Pc[s * S + sp] : 0.0;
+  }
+  if (tid == 0) {
+    int tot = 0;
+    unsigned bad = 0;
+    for (int s = 0; s < S; ++s) {
+      const int f = LO[(size_t)s * n_a + j0];
+      const int l = LO[(size_t)s * n_a + j1 - 1] - f + 2;
+      if (l < 2 || f < 0 || f + l > n_a) bad = 2u;
+      const int ll = l > 0 ? l : 0;
+      s_base[s] = tot - f;
+      s_pub[2 * s][0] = tot;
+      s_pub[2 * s][1] = tot + max(0, min(ll, j0 - f));
+      s_pub[2 * s + 1][0] = tot + min(ll, max(0, j1 - f));
+      s_pub[2 * s + 1][1] = tot + ll;
+      int* sp = &span_cl[((size_t)w * SMAX + s) * 4];
+      __hip_atomic_store(&sp[0], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[1], ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sp[2], tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot += ll;
+    }
+    s_tot = tot;
+    if (tot > cap) bad = 2u;
+    if (bad) __hip_atomic_store(r.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  auto barrier = [&]() -> bool {
+    ++nb;
+    return hc_barrier(r.err, ctr, (unsigned)G * nb, &s_flag);
+  };
+  if (!barrier()) return -1;
+  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  __syncthreads();
+  if (s_stop) return -1;
+  if (tid < S) {
+    const int s = tid;
+    int n = 0, bad = 0;
+    for (int w2 = 0; w2 < G; ++w2) {
+      const int* sp = &span_cl[((size_t)w2 * SMAX + s) * 4];
+      const int f = __hip_atomic_load(&sp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int l = __hip_atomic_load(&sp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (f < j1 && f + l > j0) {
+        const int base = __hip_atomic_load(&sp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, base};
+        else bad = 1;
+        ++n;
+      }
+    }
+    s_ncand[s] = n < kHcCand ? n : kHcCand;
+    if (bad) {
+      __hip_atomic_store(r.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  const int total = s_tot;
+  for (int q = tid; q < total; q += TH) Tacc[q] = 0.0;
+  if (!barrier()) return -1;
+  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  __syncthreads();
+  if (s_stop) return -1;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int d = j0 + tid + k * TH;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      int cf = 0, cn = 0;
+      if (s < S && d < j1) {
+        const int nc = s_ncand[s];
+        for (int c = 0; c < nc; ++c) {
+          const HcCand cd = s_cand[s][c];
+          if (d >= cd.first && d < cd.first + cd.len) {
+            if (cn == 0) cf = c;
+            ++cn;
+          }
+        }
+      }
+      s_cinfo[(k * SMAX + s) * TH + tid] = (unsigned short)(cf | (cn << 8));
+    }
+  }
+  constexpr bool kLoReg = SMAX <= 8 && KC == 1;   // with two columns per thread the registers hold the Krylov vectors
+  int dreg[KC][kLoReg ? SMAX : 1];
+  double wreg[KC][kLoReg ? SMAX : 1];
+  if constexpr (kLoReg) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = j0 + tid + k * TH;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const bool ok = s < S && j < j1;
+        dreg[k][s] = ok ? LO[(size_t)s * n_a + j] : -1;
+        wreg[k][s] = ok ? WL[(size_t)s * n_a + j] : 0.0;
+      }
+    }
+  }
+  const int v_base = lane < S ? s_base[lane] : 0;
+  const int v_plo = lane < 2 * S ? s_pub[lane][0] : 0;
+  const int v_phi = lane < 2 * S ? s_pub[lane][1] : 0;
+  // the column index is re-materialised per phase through an empty asm: otherwise the
+  // compiler hoists every point's address, hash and predicate out of the loop and keeps
+  // them live across the gathers (hundreds of VGPRs of spills)
+  const int jbase = j0 + tid;
+  auto col = [&]() {
+    int c = jbase;
+    asm volatile("" : "+v"(c));
+    return c;
+  };
+
+  // ---- the matvec pieces ----
+  // push q's own sources into the LDS spans (np.add.at(T[s], lo, wlo q) and lo + 1)
+  auto push = [&](const double (&q)[KC][SMAX]) {
+    // lottery rows in groups whose loads (L2) are all in flight before the first atomic
+    constexpr int PR = SMAX <= 8 ? SMAX : 4;
+    const int jc = col();   // lottery addresses formed here, not hoisted (they spilled)
+#pragma unroll
+    for (int s0 = 0; s0 < SMAX; s0 += PR) {
+      if (s0 < S) {
+        int dd[KC][PR];
+        double ww[KC][PR];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int j = jc + k * TH;
+#pragma unroll
+          for (int u = 0; u < PR; ++u) {
+            const int s = s0 + u;
+            if constexpr (kLoReg) {
+              dd[k][u] = s < SMAX ? dreg[k][s < SMAX ? s : 0] : -1;
+              ww[k][u] = s < SMAX ? wreg[k][s < SMAX ? s : 0] : 0.0;
+            } else {
+              // unconditional loads at a clamped index (no exec-masked branch per load)
+              const bool ok = s < S && j < j1;
+              const int q = min(s, S - 1) * n_a + min(j, n_a - 1);
+              const int dv = LO[q];
+              const double wv = WL[q];
+              dd[k][u] = ok ? dv : -1;
+              ww[k][u] = ok ? wv : 0.0;
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const bool act = j0 + tid + k * TH < j1;
+#pragma unroll
+          for (int u = 0; u < PR; ++u) {
+            const int s = s0 + u;
+            if (s < S) {   // wave-uniform
+              const int d = dd[k][u];
+              const double vlo = ww[k][u] * q[k][s];          // np.add.at(T[s], lo, wlo q)
+              const double vhi = (1.0 - ww[k][u]) * q[k][s];  // np.add.at(T[s], lo + 1, (1 - wlo) q)
+              const int ilo = __builtin_amdgcn_readlane(v_base, s) + d, ihi = ilo + 1;
+              const int d0 = __builtin_amdgcn_readfirstlane(d);
+              if (__all(act && d == d0)) {   // the whole wave on one destination (borrowing constraint)
+                const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
+                if (lane == kWave - 1) {
+                  atomicAdd(&Tacc[ilo], tl);
+                  if (th != 0.0) atomicAdd(&Tacc[ihi], th);
+                }
+              } else if (act) {
+                if (vlo != 0.0) atomicAdd(&Tacc[ilo], vlo);
+                if (vhi != 0.0) atomicAdd(&Tacc[ihi], vhi);
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+  // publish the foreign parts of the spans write-through to slab `par`, re-zero them
+  auto publish = [&](int par) {
+    double* slab = slab_cl + ((size_t)w * 2 + par) * cap;
+    for (int rr = 0; rr < 2 * S; ++rr) {
+      const int lo = __builtin_amdgcn_readlane(v_plo, rr), hi = __builtin_amdgcn_readlane(v_phi, rr);
+      for (int q = lo + tid; q < hi; q += TH) {
+        store_f64_agent(&slab[q], Tacc[q]);
+        Tacc[q] = 0.0;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // gather the own destinations (ascending covering workgroup) and mix: Tq[k][s'] =
+  // sum_s P[s, s'] T_s[d]
+  auto gather_mix = [&](int par, double (&out)[KC][SMAX]) {
+    constexpr int GR = 4;
+    double T[KC][SMAX];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) T[k][s] = 0.0;
+    bool more = false;
+#pragma unroll
+    for (int s0 = 0; s0 < SMAX; s0 += GR) {
+      if (s0 < S) {
+        double v0[KC][GR], v1[KC][GR];
+        int oq[KC][GR];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const int d = j0 + tid + k * TH;
+#pragma unroll
+          for (int q = 0; q < GR; ++q) {
+            const int s = s0 + q;
+            v0[k][q] = 0.0;
+            v1[k][q] = 0.0;
+            oq[k][q] = -1;
+            if (s < S) {
+              const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+              if (cn >= 1) {
+                const HcCand c = s_cand[s][cf];
+                if (c.w != w) v0[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
+              }
+              if (cn >= 2) {
+                const HcCand c = s_cand[s][cf + 1];
+                if (c.w != w) v1[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
+                else oq[k][q] = c.base + d;
+              }
+              more = more || cn > 2;
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int q = 0; q < GR; ++q)
+            if (oq[k][q] >= 0) {
+              T[k][s0 + q] = Tacc[oq[k][q]];
+              Tacc[oq[k][q]] = 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int q = 0; q < GR; ++q) T[k][s0 + q] = (v0[k][q] + v1[k][q]) + T[k][s0 + q];
+      }
+    }
+    if (__any(more)) {   // columns covered by more than two spans (the borrowing constraint)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const int d = j0 + tid + k * TH;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          if (s < S) {
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+            for (int c0 = 2; c0 < cn; c0 += 4) {
+              double x[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u;
+                x[u] = 0.0;
+                if (c < cn) x[u] = hc_take(s_cand[s][cf + c], w, d, par, cap, slab_cl, Tacc);
+              }
+              T[k][s] += ((x[0] + x[1]) + x[2]) + x[3];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int sp = 0; sp < SMAX; ++sp) {
+      double pc[SMAX];
+      asm volatile("" ::: "memory");   // one column of P at a time (else all of P is hoisted)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) pc[s] = s_P[s * SMAX + sp];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) acc += pc[s] * T[k][s];
+        out[k][sp] = acc;
+      }
+    }
+  };
+  // one matvec: out = T q (the cluster exchange in the middle)
+  auto matvec = [&](const double (&q)[KC][SMAX], double (&out)[KC][SMAX]) -> bool {
+    HK_PH(5);
+    push(q);
+    HK_PH(0);
+    const int par = (int)((nb + 1) & 1);
+    publish(par);
+    HK_PH(1);
+    if (!barrier()) return false;
+    HK_PH(2);
+    gather_mix(par, out);
+    HK_PH(3);
+    return true;
+  };
+  // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
+  // fixed order at every level, so every workgroup gets the same s_res
+  // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
+  // fixed order at every level, so every workgroup gets the same s_res.  The workgroup's
+  // values travel as tagged 8-byte granules ({epoch, 32 data bits}, two per double, sc1
+  // stores; MI355X_MICROARCH.md hand-off R2): the data is its own flag, so there is no
+  // counter barrier and no store drain -- wave 0 re-reads the cluster's granules until
+  // every tag carries this reduction's epoch.  Epochs count up from 1 within a launch (the
+  // host zeroes the granules before each launch); slots alternate by epoch parity, and a
+  // matvec barrier separates any two reductions, so a slot is rewritten only after every
+  // workgroup has read it.
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, auto&& prefetch) -> bool {
+    HK_PH(5);
+#pragma unroll
+    for (int v = 0; v < kHkRed; ++v) {
+      if (v < nv) {
+        const double x = (kmax >> v) & 1u ? wave_nan_max(vals[v]) : wave_sum_lane63(vals[v]);
+        if (lane == kWave - 1) s_part[v][wid] = x;
+      }
+    }
+    __syncthreads();
+    ++ne;
+    const unsigned long long tag = (unsigned long long)ne << 32;
+    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
+    if (tid < nv) {
+      const int v = tid;
+      double x = s_part[v][0];
+      for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
+      const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+      unsigned long long* g = slot + (size_t)w * (2 * kHkRed) + 2 * v;
+      __hip_atomic_store(g, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 1, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    prefetch();   // loads the step after the reduction needs, in flight across the sweep
+    if (wid == 0) {
+      double xa[kHkRed], xb[kHkRed];
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok;
+      do {   // every granule load of a pass in flight before the tag test
+        ok = true;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int w2 = lane + u * kWave;
+#pragma unroll
+          for (int v = 0; v < kHkRed; ++v) {
+            double x = 0.0;
+            if (v < nv && w2 < G) {
+              const unsigned long long* g = slot + (size_t)w2 * (2 * kHkRed) + 2 * v;
+              const unsigned long long hi = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long lo = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
+              x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            }
+            if (u == 0) xa[v] = x;
+            else xb[v] = x;
+          }
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+          if (lane == 0) __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      } while (true);
+      if (lane == 0) s_flag = ok ? 1 : 0;
+#pragma unroll
+      for (int v = 0; v < kHkRed; ++v) {
+        if (v < nv) {
+          const bool mx = (kmax >> v) & 1u;
+          const double y = mx ? wave_nan_max(nan_max(xa[v], xb[v])) : wave_sum_lane63(xa[v] + xb[v]);
+          if (lane == kWave - 1) s_res[v] = y;
+        }
+      }
+    }
+    __syncthreads();
+    HK_PH(4);
+    return s_flag != 0;
+  };
+
+  // ---- BiCGSTAB ----
+  // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
+  // p in the HBM scratch row across the second matvec, whose gather needs the registers
+  double rv[KC][SMAX], pv[KC][SMAX], tv[KC][SMAX];
+  // v: in LDS behind the spans when it fits (SMAX <= 8), else a per-workgroup HBM block of
+  // the same [KC][SMAX][TH] layout (behind the p rows of the scratch)
+  double* Vl = kVlds ? Tacc + cap : r.Vg;
+  double* Pg = r.Pg;
+  auto vidx = [&](int k, int s) { return (k * SMAX + s) * TH + tid; };
+  double part[kHkRed];
+  const double tol = r.tol;
+  int mv = 0;                 // matvecs
+  bool restart = true, first = true;
+  double rho = 0.0, total0 = 0.0;
+  auto own = [&](int jc, int k, int s) { return s < S && jc + k * TH < j1; };
+  unsigned seed = 0;   // shadow-residual choice; a stagnating solve restarts with the next one
+  auto rh_at = [&](int jc, int k, int s) { return hk_rhat((unsigned)(s * n_a + jc + k * TH) + seed * 0x5BD1E995u); };
+  double best = __builtin_inf();   // best recursive max|r| since the last restart, and when
+  int mv_best = 0;
+  auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
+  HK_PH(-1);
+  while (true) {
+    if (restart) {
+      // true residual of x: pv = x, tv = T x, rv = T x - x
+      int jc = col();
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          const double xv = X[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
+          pv[k][s] = own(jc, k, s) ? xv : 0.0;
+        }
+      if (!matvec(pv, tv)) return -1;
+      ++mv;
+      jc = col();
+      double rr = 0.0, rm = 0.0, xs = 0.0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          rv[k][s] = tv[k][s] - pv[k][s];
+          if (own(jc, k, s)) {
+            rr += rh_at(jc, k, s) * rv[k][s];
+            rm = nan_max(rm, fabs(rv[k][s]));
+            xs += pv[k][s];
+          }
+        }
+      part[0] = rr;
+      part[1] = rm;
+      part[2] = xs;
+      if (!reduce(part, 3, 2u, [] {})) return -1;
+      rho = s_res[0];
+      if (mv == 1) total0 = s_res[2];   // the starting mass's total
+      if (s_res[1] < tol || mv >= r.max_iter) {   // converged (np.max(...) < tol: NaN never is)
+        // T x rescaled to the start's total: the residual test cannot see the scale of x,
+        // and near a breakdown (huge alpha) rounding can move sum(x) away from it; T
+        // preserves totals, as the plain iteration does
+        const double scale = total0 / s_res[2];
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int s = 0; s < SMAX; ++s)
+            if (own(jc, k, s)) X[gidx(jc, k, s)] = mv == 1 ? tv[k][s] : tv[k][s] * scale;
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) pv[k][s] = rv[k][s];
+      restart = false;
+      first = true;
+    }
+    // v = p - T p (to LDS); alpha = rho / <rh, v>; the previous step's max|r| rides along.
+    // r waits in v's slot during this matvec (only p and the result stay in registers)
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) Vl[vidx(k, s)] = rv[k][s];
+    if (!matvec(pv, tv)) return -1;
+    ++mv;
+    int jc = col();
+    double rvv = 0.0, rm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const double v = pv[k][s] - tv[k][s];
+        rv[k][s] = Vl[vidx(k, s)];
+        Vl[vidx(k, s)] = v;
+        if (own(jc, k, s)) {
+          rvv += rh_at(jc, k, s) * v;
+          rm = nan_max(rm, fabs(rv[k][s]));
+        }
+      }
+    part[0] = rvv;
+    part[1] = rm;
+    double xq[KC][SMAX];   // x of the own points, for x += alpha p
+    if (!reduce(part, 2, 2u, [&] {
+          const int jq = col();
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
+        }))
+      return -1;
+    if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
+      restart = true;
+      continue;
+    }
+    // stagnation (BiCGSTAB can stall for a particular shadow residual: one Table II cell
+    // sat at max|r| ~ 6e-5 with the first hash): no 10 % gain in kHkStall matvecs ->
+    // restart from the true residual with the next shadow residual
+    if (first || s_res[1] < 0.9 * best) {
+      best = first ? __builtin_inf() : s_res[1];
+      mv_best = mv;
+    } else if (mv - mv_best > kHkStall) {
+      ++seed;
+      best = __builtin_inf();
+      restart = true;
+      continue;
+    }
+    first = false;
+    const double alpha = rho / s_res[0];
+    if (!(fabs(alpha) < 1e300)) {   // breakdown (<rh, v> = 0) or NaN: restart from the true residual
+      restart = true;
+      continue;
+    }
+    // x += alpha p; p -> HBM scratch; s = r - alpha v (in rv); t = s - T s (in tv)
+    jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        if (own(jc, k, s)) {
+          const int g = s * n_a + jc + k * TH;
+          X[g] = xq[k][s] + alpha * pv[k][s];
+          Pg[g] = pv[k][s];
+        }
+        rv[k][s] -= alpha * Vl[vidx(k, s)];
+      }
+    if (!matvec(rv, tv)) return -1;
+    ++mv;
+    jc = col();
+    double ts = 0.0, tt = 0.0, rs = 0.0, rt = 0.0, sm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        tv[k][s] = rv[k][s] - tv[k][s];
+        if (own(jc, k, s)) {
+          const double h = rh_at(jc, k, s);
+          ts += tv[k][s] * rv[k][s];
+          tt += tv[k][s] * tv[k][s];
+          rs += h * rv[k][s];
+          rt += h * tv[k][s];
+          sm = nan_max(sm, fabs(rv[k][s]));
+        }
+      }
+    part[0] = ts;
+    part[1] = tt;
+    part[2] = rs;
+    part[3] = rt;
+    part[4] = sm;
+    double pq[KC][SMAX];   // x and p of the own points, for x += omega s and the new p
+    if (!reduce(part, 5, 16u, [&] {
+          const int jq = col();
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+              const int g = min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1);
+              xq[k][s] = X[g];
+              pq[k][s] = Pg[g];
+            }
+        }))
+      return -1;
+    double omega = (s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1];
+    if (!(fabs(omega) < 1e300)) omega = 0.0;
+    if (omega == 0.0) {   // s already below tol (x + alpha p is the answer), or <t, t> = 0: verify
+      restart = true;
+      continue;
+    }
+    const double rho2 = s_res[2] - omega * s_res[3];
+    const double beta = (rho2 / rho) * (alpha / omega);
+    rho = rho2;
+    // x += omega s; r = s - omega t; p = r + beta (p - omega v)
+    jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const bool ow = own(jc, k, s);
+        if (ow) X[s * n_a + jc + k * TH] = xq[k][s] + omega * rv[k][s];
+        const double pold = ow ? pq[k][s] : 0.0;
+        rv[k][s] = rv[k][s] - omega * tv[k][s];
+        pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
+      }
+    if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
+  }
+#ifdef AIY_DIAG_PHASES
+  if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10 && mv > 0)
+    printf("[bicg phases] block %d G=%d nj=%d matvecs=%d us/matvec: push %.2f publish %.2f barrier %.2f gather+mix "
+           "%.2f reduce %.2f vector %.2f\n",
+           (int)blockIdx.x, G, j1 - j0, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv, ph[3] * 0.01 / mv,
+           ph[4] * 0.01 / mv, ph[5] * 0.01 / mv);
+#endif
+  return mv;
+}
+
+}  // namespace aiy

@@ -45,7 +45,7 @@ struct HcCand {
 
 // Cluster barrier: lane 0 adds one to the cluster counter (after the caller's drained sc1
 // stores) and waits until it reaches `target`.  False on timeout (error word set).
-__device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsigned target, int* s_flag) {
+__device__ __forceinline__ bool hc_barrier(unsigned* err, unsigned* ctr, unsigned target, int* s_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -54,11 +54,45 @@ __device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsign
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
       }
     }
+    *s_flag = ok;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+__device__ __forceinline__ bool hc_barrier(const HcRun& r, unsigned* ctr, unsigned target, int* s_flag) {
+  return hc_barrier(r.err, ctr, target, s_flag);
+}
+
+// Cluster barrier that also counts the workgroups whose `flag` is set: lane 0 adds
+// (1 | flag << 32) to the 64-bit word of the barrier's parity (low half: arrivals, high
+// half: cumulative flags of that parity; a workgroup can run at most one barrier ahead, so
+// the other parity's word takes its early add) and waits for `target` arrivals (G times
+// the barriers of this parity so far).  *nc_out: the flag count of this parity after every
+// workgroup's add.  False on timeout (error word set).
+__device__ __forceinline__ bool hc_barrier_count(unsigned* err, unsigned long long* cw, unsigned target,
+                                                 unsigned flag, unsigned* nc_out, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long v = __hip_atomic_fetch_add(cw, 1ull | ((unsigned long long)flag << 32), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) +
+                           (1ull | ((unsigned long long)flag << 32));
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while ((unsigned)v < target) {
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *nc_out = (unsigned)(v >> 32);
     *s_flag = ok;
   }
   __syncthreads();

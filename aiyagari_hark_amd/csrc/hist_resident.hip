@@ -52,37 +52,6 @@ namespace aiy {
   } while (0)
 #endif
 
-// Cluster barrier of iteration `it` that also counts the workgroups whose last change was
-// not below tol: lane 0 adds (1 | flag << 32) to the 64-bit word of the iteration's parity
-// (low half: arrivals, high half: cumulative flags of that parity; a workgroup can run at
-// most one barrier ahead, so the other parity's word takes its early add) and waits for
-// G * (barriers of this parity so far) arrivals.  *nc_out: the flag count of this parity
-// after every workgroup's add.  False on timeout (error word set).
-__device__ __forceinline__ bool hc_barrier_count(const HcRun& r, unsigned long long* cw, unsigned target,
-                                                 unsigned flag, unsigned* nc_out, int* s_flag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long v = __hip_atomic_fetch_add(cw, 1ull | ((unsigned long long)flag << 32), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) +
-                           (1ull | ((unsigned long long)flag << 32));
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int ok = 1;
-    while ((unsigned)v < target) {
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    *nc_out = (unsigned)(v >> 32);
-    *s_flag = ok;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
-
 template <int SMAX, int KC, int TH>
 __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 #ifdef AIY_DIAG_PHASES
@@ -331,7 +300,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     // the barrier carries the stop test: flag = change of mix it - 1 not below tol (NaN
     // included, as np.max(...) < tol is False for NaN)
     const unsigned flag = (it >= 2 && dloc < r.tol) ? 0u : 1u;
-    if (!hc_barrier_count(r, &cw[par], (unsigned)G * (unsigned)((it + par) / 2), flag, &s_nc, &s_flag)) return;
+    if (!hc_barrier_count(r.err, &cw[par], (unsigned)G * (unsigned)((it + par) / 2), flag, &s_nc, &s_flag)) return;
     HC_PH(3);
     // ---- gather own destinations from the covering spans (ascending w): foreign ones from
     // their slabs, the own one from LDS ----
@@ -586,8 +555,14 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
   const size_t stat = fa.sharedSizeBytes;
-  if (stat + 4096 >= kHcLdsTotal) return false;
-  p.lds = (kHcLdsTotal - stat - 1024) / 256 * 256;
+  // the LDS budget is the device's own (160 KB per CU on gfx950; an arch override with
+  // less LDS makes the plan not fit instead of failing the attribute call below)
+  int lds_dev = 0;
+  if (hipDeviceGetAttribute(&lds_dev, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess)
+    return false;
+  const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
+  if (stat + 4096 >= lds_total) return false;
+  p.lds = (lds_total - stat - 1024) / 256 * 256;
   // BiCGSTAB: one resident vector (v, [KC][SMAX][TH] doubles) behind the span buffer
   const size_t vbytes = krylov && smax_k <= 8 ? (size_t)p.kc * smax_k * p.th * sizeof(double) : 0;
   p.vblock = krylov && smax_k > 8 ? (size_t)p.kc * smax_k * p.th : 0;   // v in HBM, doubles per workgroup
@@ -619,9 +594,17 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   HcPlan p;
   const bool krylov = h->hist_krylov != 0;
   if (!hc_make_plan(h, n_cal, S, n_a, p, krylov)) return AIY_ERR_UNSUPPORTED;
-  AIY_HIP(h, hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
+  // a launch shape the device does not admit is "unsupported" (the caller's push/mix
+  // fallback runs), not a hard error
+  if (hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return AIY_ERR_UNSUPPORTED;
+  }
   int per_cu = 0;
-  AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds));
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return AIY_ERR_UNSUPPORTED;
+  }
   if (per_cu < 1) return AIY_ERR_UNSUPPORTED;
   const int per_launch = std::min(n_cal, p.cals_per_launch);
   int32_t rc = hc_scratch(h, per_launch, p.G, p.cap);

@@ -55,6 +55,14 @@ struct aiy_handle {
   hipEvent_t hc_ev[2] = {nullptr, nullptr};
   double hc_ms_sum = 0.0;
   long long hc_launches = 0;
+  // device-resident GE search (ge_resident.hip)
+  bool ge_resident = false;          // AIY_OPT_GE_RESIDENT
+  int cu_limit = 0;                  // AIY_OPT_CU_LIMIT: compute units resident launches may fill (0: all)
+  void* d_ge = nullptr;              // tables, masses, lottery, cluster sync of the launch
+  size_t ge_cap = 0;
+  hipEvent_t ge_ev[2] = {nullptr, nullptr};
+  double ge_ms_sum = 0.0, ge_points = 0.0, ge_egm_cycles = 0.0;
+  long long ge_launches = 0;
   // wealth statistics (stats.hip): sort / scan scratch
   void* d_stats = nullptr;
   size_t stats_cap = 0;
@@ -94,6 +102,9 @@ int32_t launch_build_index(aiy_handle* h, const double* x, long long n_rows, int
 int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int* lo, const double* wlo,
                             const double* P, double tol, int max_iter, double* mass, int* d_iters, hipStream_t st);
 int32_t hist_resident_plan(aiy_handle* h, int n_cal, int S, int n_a, int* out4);
+int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, const aiy_ge_options* o, double* r_out,
+                               double* K_out, double* Ks_out, int32_t* steps_out, int32_t* cyc_out,
+                               int32_t* its_out, int32_t* status_out, hipStream_t st);
 
 inline int32_t fail(aiy_handle* h, int32_t code, const char* fmt, ...) {
   char buf[512];

@@ -456,6 +456,11 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       h->hist_accel = (int)value;
       return AIY_OK;
     case AIY_OPT_HIST_KRYLOV: h->hist_krylov = value != 0; return AIY_OK;
+    case AIY_OPT_GE_RESIDENT: h->ge_resident = value != 0; return AIY_OK;
+    case AIY_OPT_CU_LIMIT:
+      if (value < 0 || value > 65536) return fail(h, AIY_ERR_ARG, "AIY_OPT_CU_LIMIT must be in [0, 65536]");
+      h->cu_limit = (int)value;
+      return AIY_OK;
     case AIY_OPT_HIST_CLUSTER:
       if (value < 0 || value > 128) return fail(h, AIY_ERR_ARG, "AIY_OPT_HIST_CLUSTER must be in [0, 128]");
       h->hist_cluster_cap = (int)value;

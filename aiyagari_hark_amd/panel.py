@@ -113,7 +113,7 @@ class DevicePanel:
         sp = _lib.stream_ptr(stream)
         if allreduce is not None:
             self._run_stepwise(h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
-                               allreduce, emp_source)
+                               allreduce, emp_source, stream)
             return
         if self._engine(h) == "block":
             if self.n_total != self.n_local or self.agent_offset != 0:
@@ -147,10 +147,13 @@ class DevicePanel:
             t += n
 
     def _run_stepwise(self, h, pm, mk, t0, n_periods, shock_mode, seed, ge_iter, u_host_source, chunk, sp,
-                      allreduce, emp_source=None):
+                      allreduce, emp_source=None, stream=None):
         """Sharded periods with the all-reduce done by the caller between the library's two
         steps (Aiyagari_Support.py:1868, np.mean over all ranks' agents)."""
         red = self.sow[6:7]
+        # the all-reduce runs on the stream the library steps were enqueued on (the nccl
+        # backend enqueues on torch's current stream, the gloo path syncs it before its copy)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
         t, end = t0, t0 + n_periods
         while t < end:
             n = min(chunk, end - t)
@@ -164,12 +167,13 @@ class DevicePanel:
                                                    _lib.ptr(self.a), _lib.ptr(self.lab), up, ep,
                                                    int(seed) & ((1 << 64) - 1), int(ge_iter), int(t + k),
                                                    _lib.ptr(self.sow), sp), "aiy_sim_period_local")
-                allreduce(red)
+                with torch.cuda.stream(st):
+                    allreduce(red)
                 h.check(h.lib.aiy_sim_period_prices(h.h, ctypes.byref(pm), ctypes.byref(mk), self.n_total, int(t + k),
                                                     _lib.ptr(self.sow), _lib.ptr(self.hist_A), _lib.ptr(self.hist_M),
                                                     sp), "aiy_sim_period_prices")
             if ud is not None or ed is not None:
-                torch.cuda.current_stream(self.device).synchronize()
+                st.synchronize()
             del ud, ed
             t += n
 

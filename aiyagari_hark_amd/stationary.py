@@ -65,6 +65,17 @@ def table2_calibrations(**kw):
             for s in TABLE2_SIGMA for r in TABLE2_RHO for c in TABLE2_CRRA]
 
 
+def _resolve_device(device):
+    """torch.device with an explicit index: None / "cuda" mean the current device (library
+    handles are per device index, _lib.Handle(dev.index))."""
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError(f"stationary solves run on a GPU, not {dev}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
 def firm_prices(r, alpha, delta):
     """(w, K_demand) with L = 1 (Cobb-Douglas firm of calc_R_and_W, AS:1886-1890)."""
     KtoL = (alpha / (r + delta)) ** (1.0 / (1.0 - alpha))
@@ -81,6 +92,9 @@ class StationaryResult:
     bisection_steps: int
     egm_cycles: list = field(default_factory=list)
     hist_iters: list = field(default_factory=list)
+    # per calibration (native engine): bit 1 a household solve stopped at its cycle cap,
+    # bit 2 a distribution solve at its iteration cap, bit 4 the search at max_steps
+    status: np.ndarray | None = None
 
 
 class StationaryBatch:
@@ -88,7 +102,7 @@ class StationaryBatch:
 
     def __init__(self, cals, aGrid, device=None):
         self.cals = list(cals)
-        self.device = torch.device(device or "cuda")
+        self.device = _resolve_device(device)
         n_cal = len(self.cals)
         levels, Ps = zip(*(c.income_process() for c in self.cals))
         S = len(levels[0])
@@ -262,14 +276,17 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
                          int(max_steps), 5000, 200000, int(bool(warm_hist)), int(bool(warm_egm)), int(accel),
                          ctypes.addressof(lo) if lo is not None else None,
                          ctypes.addressof(hi) if hi is not None else None, int(bool(secant)), int(bool(loose)),
-                         int(bool(extrapolate)))
+                         int(bool(extrapolate)), None)
+    status = (ctypes.c_int32 * n)()
+    opt.status_out = ctypes.addressof(status)
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
                                     ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its),
                                     _lib.stream_ptr(stream)),
             "aiy_ge_stationary")
-    return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value))
+    return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value),
+            np.array(status[:], dtype=np.int32))
 
 
 _GROUP_CTX = {}   # (device, group) -> (library handle, torch stream), reused across sweeps
@@ -285,8 +302,15 @@ def _close_groups():
 atexit.register(_close_groups)
 
 
+def _device_cus(dev, cu_share=1.0):
+    """Compute units this process may fill with resident clusters: the device's, times
+    cu_share (< 1 when several rank processes share one GPU, the bench's gloo rehearsal)."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return max(1, int(cus * float(cu_share)))
+
+
 def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel,
-                  r_lo, r_hi, secant, loose, extrapolate):
+                  r_lo, r_hi, secant, loose, extrapolate, cu_share=1.0):
     """Independent root searches for `groups` subsets of the calibrations, each on its own
     library handle and stream from its own host thread (the library releases the GIL):
     a batched search steps all its calibrations together and pays, at every step, for its
@@ -300,7 +324,7 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
     # measured 177 GE solves/s, contiguous (sigma, rho) blocks 176, round-robin 204)
     idx = [list(range(g, n, groups)) for g in range(groups)]
     idx = [i for i in idx if i]
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    cus = _device_cus(dev, cu_share)
     cap = max(1, min(32, cus // n))
     cur = torch.cuda.current_stream(dev)
     jobs = []
@@ -326,21 +350,22 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
     for _, _, _, st, _, _ in jobs:
         cur.wait_stream(st)
     r, K, Ks = np.zeros(n), np.zeros(n), np.zeros(n)
+    status = np.zeros(n, dtype=np.int32)
     steps = cyc = its = 0
-    for (ii, b, *_), (rg, Kg, Ksg, sg, cg, ig) in zip(jobs, outs):
-        r[ii], K[ii], Ks[ii] = rg, Kg, Ksg
+    for (ii, b, *_), (rg, Kg, Ksg, sg, cg, ig, stg) in zip(jobs, outs):
+        r[ii], K[ii], Ks[ii], status[ii] = rg, Kg, Ksg, stg
         steps, cyc, its = max(steps, sg), cyc + cg, its + ig
     alpha = np.array([c.CapShare for c in cals])
     delta = np.array([c.DeprFac for c in cals])
     KtoY = K ** (1.0 - alpha)
     return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=delta * KtoY, bisection_steps=steps,
-                            egm_cycles=[np.array([cyc])], hist_iters=[np.array([its])])
+                            egm_cycles=[np.array([cyc])], hist_iters=[np.array([its])], status=status)
 
 
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
                  method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None,
-                 extrapolate=None, groups=None):
+                 extrapolate=None, groups=None, cu_share=1.0):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -361,15 +386,20 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     stopping rules, fewer cycles / matvecs).  loose (native only; default: on for
     "brent"): while a calibration is still bracketing its root, its evaluations stop at
     egm 1e-6 / hist 1e-10 and their sign is used only where |K_s - K_d| >= 5 % of K_d
-    (else that r is evaluated again at the full tolerances); every evaluation Brent's
-    method interpolates from runs at the full tolerances.  extrapolate (native only;
+    (else that r is evaluated again at the full tolerances).  The two bracket endpoints
+    Brent's method starts from may be such loose evaluations (their sign is certain, their
+    value good to ~1e-6 relative); every later point is a full-tolerance evaluation, and
+    the root is still bracketed by the 5 % sign margin.  extrapolate (native only;
     default: on for "brent"): the household solves extrapolate their cycle iterates
     geometrically where the distances fall at a steady rate (csrc/egm.hip; same stopping
     rule).  groups (native only; default: 3 for "brent" with >= 3 calibrations, else 1):
     the calibrations split round-robin into independent searches on their own handles,
     streams and host threads (_solve_groups; 3 groups fill the process's hardware queues
-    beside the default stream -- 4 measured slower)."""
+    beside the default stream -- 4 measured slower).  cu_share: the fraction of the
+    device's compute units this process's resident clusters may hold (several rank
+    processes on one GPU: 1 / ranks), so that every process's clusters stay co-resident."""
     cals = table2_calibrations() if cals is None else list(cals)
+    device = _resolve_device(device)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
     if warm_egm is None:
         warm_egm = method == "brent"
@@ -389,13 +419,12 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         # times the calibrations must fit the compute units, else one batched search
         S0 = cals[0].LaborStatesNo
         g_min = -(-n_a // (512 * (2 if S0 <= 8 else 1)))
-        cus = torch.cuda.get_device_properties(torch.device(device or "cuda")).multi_processor_count
-        if g_min * len(cals) > cus:
+        if g_min * len(cals) > _device_cus(device, cu_share):
             groups = 1
     if engine == "native" and log is None and groups > 1 and len(cals) > 1:
-        return _solve_groups(cals, aGrid, torch.device(device or "cuda"), int(groups), method, r_tol, egm_tol,
+        return _solve_groups(cals, aGrid, device, int(groups), method, r_tol, egm_tol,
                              hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo, r_hi,
-                             secant and warm_hist and warm_egm, loose, extrapolate)
+                             secant and warm_hist and warm_egm, loose, extrapolate, cu_share)
     b = StationaryBatch(cals, aGrid, device=device)
     n = len(cals)
     lo = np.full(n, -0.5 * b.delta) if r_lo is None else np.broadcast_to(np.asarray(r_lo, float), (n,)).copy()
@@ -405,14 +434,14 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     cyc_log, it_log = [], []
     Ks = np.zeros(n)
     if engine == "native" and log is None:
-        r, K, Ks, steps, cyc_sum, it_sum = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
+        r, K, Ks, steps, cyc_sum, it_sum, status = ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps,
                                                                 warm_hist, warm_egm, accel, r_lo if r_lo is not None
                                                                 else None, r_hi if r_hi is not None else None,
                                                                 secant=secant and warm_hist and warm_egm,
                                                                 loose=loose, extrapolate=extrapolate)
         KtoY = K ** (1.0 - b.alpha)
         return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
-                                egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])])
+                                egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])], status=status)
     if method == "brent":
         search = [_Brent(lo[k], hi[k], r_tol) for k in range(n)]
         while not all(sr.done for sr in search) and steps < max_steps:

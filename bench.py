@@ -57,6 +57,7 @@ N_A = 10_000
 ACT_T = 11_000
 T_DISCARD = 1_000
 N_TABLE2 = 24
+N_TABLE2_CPU_CELL = 6          # (rho 0.6, sigma 0.2, CRRA 1) in stationary.table2_calibrations() order
 
 
 def log(*a):
@@ -81,18 +82,38 @@ def spawn_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
-def setup_dist():
+def setup_dist(backend="nccl"):
+    """One rank per GPU over RCCL ("nccl").  backend "gloo" is the one-GPU rehearsal of
+    the multi-rank bench: every rank on device 0 (LOCAL_RANK modulo the visible devices),
+    the rendezvous and the collectives over gloo, configs3's per-period sum through the
+    library's two-step sharded period (RCCL refuses two ranks on one device)."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
+
+
+def cu_share(world):
+    """Fraction of the GPU one rank's resident clusters may hold: 1, or 1 / ranks when the
+    gloo rehearsal puts every rank on one device."""
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        if dist.get_backend() == "gloo":
+            return 1.0 / max(1, -(-world // max(1, torch.cuda.device_count())))
+    return 1.0
 
 
 def barrier(world):
@@ -108,7 +129,8 @@ def max_over_ranks(x, world, dev):
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    on_dev = dist.get_backend() != "gloo"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -149,8 +171,10 @@ def table2_leg(args, world, rank, dev):
     cals = [cells[k] for k in mine]
     h = _lib.handle(dev.index)
 
+    share = cu_share(world)
+
     def sweep():
-        return solve_table2(cals, n_a=args.grid, device=dev, method="brent")
+        return solve_table2(cals, n_a=args.grid, device=dev, method="brent", cu_share=share)
 
     for _ in range(args.warmup):
         sweep()
@@ -317,72 +341,165 @@ def configs1_leg(args, world, rank, dev):
 # ------------------------------------------------------------------------------------
 # configs[3]: 1e8 agents x 1000 periods, agent-sharded, per-period RCCL all-reduce
 # ------------------------------------------------------------------------------------
-def configs3_leg(args, world, rank, dev, econ, agent):
-    import torch
-    from aiyagari_hark_amd import _lib
-    from aiyagari_hark_amd import setup_math as sm
-    from aiyagari_hark_amd.panel import DevicePanel
-    from aiyagari_hark_amd.parallel import bind_rccl, initial_labor_states, shard_range, unbind_rccl
-    h = _lib.handle(dev.index)
-    n_total = args.c3_agents
-    T = args.c3_periods
-    off, nl = shard_range(n_total, world, rank)
-    # the policy every rank simulates: the converged configs[1] household at the reference's
-    # initial saving rule (deterministic, identical on every rank)
+def c3_policy(dev, n_a, n_agents=N_AGENTS):
+    """The household every configs[3] rank simulates: the configs[1] economy's converged
+    policy at the reference's initial saving rule (intercept 0, slope 1; [HARK] solve_agent
+    to 1e-6 from the terminal guess) -- deterministic, identical on every rank.  Returns
+    (econ, agent) with agent.solution[0] set."""
+    econ, agent = make_economy(seed=0, n_agents=n_agents, n_a=n_a, act_T=ACT_T, device=dev)
     reset_rule(econ, agent)
     agent.solve()
+    return econ, agent
+
+
+def c3_panel(dev, econ, agent, n_total, T, world=1, rank=0):
+    """The configs[3] panel of this rank: contiguous agent range, labour states split
+    evenly by global index (parallel.initial_labor_states), a_0 = KSS, Philox keyed by
+    the global agent index.  Returns (panel, reset)."""
+    import torch
+    from aiyagari_hark_amd import setup_math as sm
+    from aiyagari_hark_amd.panel import DevicePanel
+    from aiyagari_hark_amd.parallel import initial_labor_states, shard_range
+    off, nl = shard_range(n_total, world, rank)
     sol = agent.solution[0]
     lab_level = torch.as_tensor(sm.labor_levels(agent.TauchenAux[0])).to(dev)
     lab_cdf = torch.as_tensor(sm.choice_cdf_table(agent.TauchenAux[1])).to(dev)
     hist = np.resize(np.asarray(econ.MrkvNow_hist, dtype=np.int32), T + 64)
-    if world > 1:
+    p = DevicePanel(nl, device=dev, agent_offset=off, n_total=n_total, act_T=T + 64, engine="grid")
+    p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, torch.as_tensor(hist).to(dev),
+                 econ.market_constants())
+    lab0 = initial_labor_states(n_total, 7, off, nl)
+
+    def reset():
+        p.reset(econ.KSS, lab0, econ.sow_init["Mnow"], econ.sow_init["Aprev"], 0, econ.sow_init["Rnow"],
+                econ.sow_init["Wnow"])
+
+    reset()
+    return p, reset
+
+
+C3_SEED = 11
+
+
+def configs3_leg(args, world, rank, dev):
+    import torch.distributed as dist
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.parallel import bind_rccl, torch_allreduce, unbind_rccl
+    h = _lib.handle(dev.index)
+    n_total = args.c3_agents
+    T = args.c3_periods
+    econ, agent = c3_policy(dev, args.grid)
+    # sharded: the library's own RCCL all-reduce (nccl backend) or, in the one-GPU gloo
+    # rehearsal, the two-step period with the caller's all-reduce
+    gloo = world > 1 and dist.get_backend() == "gloo"
+    allreduce = torch_allreduce() if gloo else None
+    if world > 1 and not gloo:
         bind_rccl(h)
     try:
-        p = DevicePanel(nl, device=dev, agent_offset=off, n_total=n_total, act_T=T + 64, engine="grid")
-        p.bind_model(sol.m_tab, sol.c_tab, sol.M_grid, lab_level, lab_cdf, torch.as_tensor(hist).to(dev),
-                     econ.market_constants())
-        lab0 = initial_labor_states(n_total, 7, off, nl)
-
-        def reset():
-            p.reset(econ.KSS, lab0, econ.sow_init["Mnow"], econ.sow_init["Aprev"], 0, econ.sow_init["Rnow"],
-                    econ.sow_init["Wnow"])
-
-        reset()
-        p.run(0, 64, shock_mode="philox", seed=11, ge_iter=0)   # warm-up
+        p, reset = c3_panel(dev, econ, agent, n_total, T, world, rank)
+        p.run(0, 64, shock_mode="philox", seed=C3_SEED, ge_iter=0, allreduce=allreduce)   # warm-up
         reset()
         h.check(h.lib.aiy_panel_launch_stats(h.h, None, None, None, 1), "stats reset")
         barrier(world)
         t0 = time.perf_counter()
-        p.run(0, T, shock_mode="philox", seed=11, ge_iter=0)
+        p.run(0, T, shock_mode="philox", seed=C3_SEED, ge_iter=0, allreduce=allreduce)
         barrier(world)
         el = max_over_ranks(time.perf_counter() - t0, world, dev)
         st_ms, st_n, st_per = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
         h.check(h.lib.aiy_panel_launch_stats(h.h, ctypes.byref(st_ms), ctypes.byref(st_n), ctypes.byref(st_per), 1),
                 "stats")
-        K_T = float(p.hist_A[T - 1].item())
+        K_hist = p.hist_A[:T].cpu().numpy()
+        nl = p.n_local
     finally:
-        if world > 1:
+        if world > 1 and not gloo:
             unbind_rccl(h)
     aps = n_total * T / el
     # dominant kernel: single rank -> the persistent panel streaming agents from HBM (HIP
-    # events around the launch); sharded -> per-period kernel + RCCL all-reduce + price
-    # kernel, timed on the wall clock of the whole period
+    # events around the launch); sharded -> per-period kernel + all-reduce + price kernel,
+    # timed on the wall clock of the whole period
     if world == 1 and st_n.value > 0:
         kern_ms = st_ms.value / st_n.value
         kern = "sim_resident_kernel (HBM-streaming form)"
     else:
         kern_ms = 1e3 * el
-        kern = "sim_period_kernel + ncclAllReduce + period_price_kernel (wall clock of the periods)"
+        kern = ("sim_period_kernel + " + ("gloo all-reduce (two-step period)" if gloo else "ncclAllReduce") +
+                " + period_price_kernel (wall clock of the periods)")
     bytes_launch = PANEL_BYTES_PER_AGENT * nl * T
     gbs = bytes_launch / max(1e-12, kern_ms * 1e-3) / 1e9
     out = dict(value=aps, unit="agent-periods/s", agents=n_total, periods=T, seconds=el, agents_per_rank=nl,
-               us_per_period=1e6 * el / T, K_final=K_T,
+               us_per_period=1e6 * el / T, K_final=float(K_hist[T - 1]), K_first=[float(x) for x in K_hist[:5]],
                roofline={"kernel": kern, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": kern_ms},
+                         "frac": gbs / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("sim_resident_kernel_stream") if world == 1 else None,
+                         "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": kern_ms},
                workload=f"BASELINE configs[3]: {n_total} agents x {T} periods, agents sharded over {world} rank(s), "
-                        "Philox by global agent index, per-period RCCL all-reduce of the asset sum when sharded")
+                        "Philox by global agent index, per-period all-reduce of the asset sum when sharded "
+                        f"({'gloo two-step rehearsal' if gloo else 'RCCL'})")
     log(f"[bench] configs3: {el:.3f} s for {T} periods ({aps:.3e} agent-periods/s, {1e6 * el / T:.0f} us/period)")
+    return out
+
+
+# ------------------------------------------------------------------------------------
+# configs[4]: stress -- 25-state Rouwenhorst, 50 000-point grid, Young histogram
+# ------------------------------------------------------------------------------------
+STRESS_N_A = 50_000
+
+
+def stress_calibrations():
+    from aiyagari_hark_amd.stationary import Calibration
+    return [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst")
+            for c in (1.0, 3.0, 5.0)]
+
+
+def configs4_leg(args, world, rank, dev):
+    """BASELINE configs[4]: rho 0.9, sigma 0.4, CRRA in {1, 3, 5}, 25-state Rouwenhorst
+    (E3), N_a = 50 000, each solved to GE in r with the bench's Table II options; the
+    three cells split round-robin over the ranks.  Dominant kernel: the 25-state
+    BiCGSTAB distribution solve (98 workgroups per calibration, v in HBM)."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.parallel import split_calibrations
+    from aiyagari_hark_amd.stationary import solve_table2
+    cells = stress_calibrations()
+    mine = split_calibrations(list(range(len(cells))), world, rank)
+    cals = [cells[k] for k in mine]
+    h = _lib.handle(dev.index)
+    n_a = args.stress_grid
+
+    share = cu_share(world)
+
+    def solve():
+        return solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share) if cals else None
+
+    solve()   # warm-up
+    hist_stats(h, True, dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    res = solve()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    hist_ms, hist_n = hist_stats(h, True, dev)
+    pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
+    hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
+    gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
+    per_rank = gather_objects(dict(cells=mine, r=[] if res is None else [float(x) for x in res.r],
+                                   status=[] if res is None else [int(x) for x in res.status]), world)
+    r = [None] * len(cells)
+    st = [None] * len(cells)
+    for pr in per_rank:
+        for k, rr, ss in zip(pr["cells"], pr["r"], pr["status"]):
+            r[k], st[k] = rr, ss
+    out = dict(value=len(cells) / el, unit="GE solves/s", seconds=el, calibrations=len(cells), n_a=n_a, S=25,
+               r_percent=[round(100 * x, 6) for x in r], status=st,
+               roofline={"kernel": "hist_bicg_kernel<25, 1, 512> (BiCGSTAB distribution solve, v in HBM)",
+                         "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": hist_bytes / max(1, hist_n),
+                         "avg_launch_ms": hist_ms / max(1, hist_n), "launches": hist_n,
+                         "kernel_time_share": hist_ms * 1e-3 / max(1e-12, el)},
+               workload="BASELINE configs[4]: rho 0.9, sigma 0.4, CRRA {1,3,5}, 25-state Rouwenhorst, N_a = "
+                        f"{n_a}, stationary GE in r (Brent, the Table II options), Young histogram by BiCGSTAB")
+    log(f"[bench] configs4: {el:.3f} s for {len(cells)} stress cells ({out['value']:.2f} GE solves/s); "
+        f"hist {hist_ms:.1f} ms in {hist_n} launches, {gbs:.0f} GB/s algorithmic")
     return out
 
 
@@ -425,17 +542,36 @@ def pmc_traffic(kernel, scale=None):
 # ------------------------------------------------------------------------------------
 # CPU baseline: the oracle on this host (bounded sample of the headline workload)
 # ------------------------------------------------------------------------------------
-def _cpu_eval(args_tuple):
-    """One complete K_s(r) evaluation (EGM to 1e-8 + lottery + distribution to 1e-12) of
-    one Table II calibration at N_a = 10 000 with the vectorised NumPy oracle."""
-    rho, sig, mu, r, n_a = args_tuple
+def _cpu_ge_solve(args_tuple):
+    """One complete oracle GE solve (oracle/stationary.py ge_bisect: bisection of
+    [-delta/2, 1/beta - 1) to 1e-7, every evaluation a cold EGM to 1e-8 and a cold Young
+    histogram to 1e-12 from the uniform mass) of one Table II calibration."""
+    rho, sig, mu, n_a = args_tuple
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import stationary as ST
     aGrid = ST.make_stationary_grid(0.001, 50.0, n_a, 2)
     lab, P = ST.income_process(7, rho, sig, "tauchen")
     t = time.perf_counter()
-    K, info = ST.capital_supply(r, dict(DiscFac=0.96, CRRA=mu, CapShare=0.36, DeprFac=0.08), aGrid, lab, P, fast=True)
-    return time.perf_counter() - t, info["cycles"], info["hist_iters"]
+    g = ST.ge_bisect(dict(DiscFac=0.96, CRRA=mu, CapShare=0.36, DeprFac=0.08), aGrid, lab, P, r_tol=1e-7, fast=True)
+    return time.perf_counter() - t, g["r"], g["iters"]
+
+
+def _cpu_ks_iteration(agents=350, act_T=ACT_T):
+    """One GE iteration of the reference's own algorithm, restated by the oracle
+    (oracle/hark_ks.py KSModel: [HARK] solve_agent of the KS-form household on the
+    notebook's grids, then Market.make_history over act_T periods of `agents` agents with
+    the global-RNG labour draws, Aiyagari_Support.py:1217-1415, 1839-1894) for the
+    notebook's calibration (rho 0.3, sigma 0.2, CRRA 1; Aiyagari-HARK.ipynb:292-328)."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import hark_ks as H
+    cal = dict(LaborAR=0.3, LaborSD=0.2, CRRA=1.0)
+    m = H.KSModel(dict(cal), dict(cal, AgentCount=agents))
+    t = time.perf_counter()
+    mt, ct, cycles, _ = m.solve_agent()
+    t1 = time.perf_counter()
+    m.make_history(mt, ct, H.numpy_global_u_source(0, agents), ge_iter=0, act_T=act_T)
+    t2 = time.perf_counter()
+    return t2 - t, t1 - t, t2 - t1, cycles
 
 
 def host_info():
@@ -454,45 +590,50 @@ def host_info():
     return model, os.cpu_count(), usable
 
 
-def cpu_baseline(n_a, r_star, budget_workers=16):
-    """The oracle (oracle/stationary.py, vectorised NumPy: np.bincount lottery push, one
-    thread) on this host, on complete units of the headline workload: K_s(r) evaluations of
-    Table II calibrations at N_a = 10 000 (EGM to 1e-8, Young lottery to 1e-12).  A CPU GE
-    solve is the oracle's own bisection: 20 evaluations of the bracket [-delta/2,
-    1/beta - 1) to 1e-7, of which the first three lie far below the root (fast: the
-    distribution converges quickly) and the other 17 within ~0.5 % of it (slow).  Single
-    core, rho = 0.6 / sigma = 0.2 / CRRA = 1 cell (root r* from the GPU sweep): one
-    evaluation at r* - 2 % for the far steps and three at r* - 0.25 %, r* - 0.03 %,
-    r* + 0.005 % for the near ones; GE solve time = 3 t_far + 17 mean(t_near).  All cores:
-    one near-root evaluation (r* - 0.03 %) of each of min(usable cores, 24) cells at once in
-    a process pool, GE solves/s = cells / (20 x wall)."""
+CPU_CELL = (0.6, 0.2, 1.0)   # the BASELINE configs[0] calibration (Aiyagari_Support.py:752-755)
+
+
+def cpu_baseline(n_a, r_gpu, budget_workers=16, ks_ge_iterations=None):
+    """The oracle on this host's cores, timed on complete units of work:
+      value     -- one complete oracle GE solve (ge_bisect, 20 cold K_s(r) evaluations)
+                   of the configs[0] calibration at the bench's grid, one core
+                   (OMP_NUM_THREADS=1);
+      all_cores -- the same solve in `workers` processes at once (the GPU box's CPU share
+                   per GPU: 16; gpurun caps worker pools there), GE solves/s = workers /
+                   wall;
+      ks_reference -- one GE iteration of the reference's own Krusell-Smith algorithm
+                   (oracle KSModel, 350 agents x 11 000 periods, the notebook's run), one
+                   core, beside the GPU's table2_reference leg.
+    kind "port": the oracle is a NumPy restatement (HARK is absent)."""
     import multiprocessing as mp
     model, n_cpu, usable = host_info()
-    rs = r_star[6]   # the (0.6, 0.2, 1) cell
-    far = _cpu_eval((0.6, 0.2, 1.0, rs - 0.02, n_a))
-    near = [_cpu_eval((0.6, 0.2, 1.0, rs + dr, n_a)) for dr in (-0.0025, -0.0003, 0.00005)]
-    t_ge = 3 * far[0] + 17 * float(np.mean([o[0] for o in near]))
-    from aiyagari_hark_amd.stationary import table2_calibrations
-    cells = table2_calibrations()
-    workers = max(1, min(budget_workers, usable, len(cells)))
-    jobs = [(c.LaborAR, c.LaborSD, c.CRRA, r_star[k] - 0.0003, n_a) for k, c in enumerate(cells[:workers])]
+    t_one, r_one, steps = _cpu_ge_solve(CPU_CELL + (n_a,))
+    workers = max(1, min(budget_workers, usable))
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(workers) as pool:
-        res = pool.map(_cpu_eval, jobs)
+        res = pool.map(_cpu_ge_solve, [CPU_CELL + (n_a,)] * workers)
     all_wall = time.perf_counter() - t0
-    return {"value": 1.0 / t_ge, "unit": "GE solves/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/stationary.py (vectorised NumPy, one thread, OMP_NUM_THREADS=1) on this host: 4 "
-                       f"complete K_s(r) evaluations of the rho=0.6 sigma=0.2 CRRA=1 Table II cell at N_a={n_a}: "
-                       f"r*-2% {far[0]:.2f} s, near-root {[round(o[0], 2) for o in near]} s (histogram iterations "
-                       f"{[far[2]] + [o[2] for o in near]}); GE solve = the oracle's 20 bisection evaluations "
-                       f"(3 far + 17 near) = {t_ge:.1f} s"),
+    t_it, t_egm, t_hist, cyc = _cpu_ks_iteration()
+    ks = {"value": 1.0 / t_it, "unit": "GE iterations/s", "cores": 1, "kind": "port",
+          "sample": (f"oracle/hark_ks.py KSModel, notebook calibration (rho 0.3, sigma 0.2, CRRA 1), 32-pt grid x 15 "
+                     f"M nodes x 28 states, 350 agents x {ACT_T} periods: one GE iteration = solve_agent "
+                     f"({cyc} cycles, {t_egm:.2f} s) + make_history ({t_hist:.2f} s) = {t_it:.2f} s")}
+    if ks_ge_iterations:
+        ks["ge_solves_per_s"] = 1.0 / (t_it * float(np.mean(ks_ge_iterations)))
+        ks["ge_solves_note"] = (f"x the mean GE iteration count of the GPU table2_reference leg "
+                                f"({float(np.mean(ks_ge_iterations)):.1f})")
+    return {"value": 1.0 / t_one, "unit": "GE solves/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/stationary.py ge_bisect (vectorised NumPy, OMP_NUM_THREADS=1) of the Table II cell "
+                       f"rho={CPU_CELL[0]} sigma={CPU_CELL[1]} CRRA={CPU_CELL[2]} at N_a={n_a}: {steps} cold K_s(r) "
+                       f"evaluations, {t_one:.1f} s; r = {100 * r_one:.6f} % (GPU sweep: {100 * r_gpu:.6f} %)"),
             "host": {"cpu_model": model, "nproc": n_cpu, "usable_cores": usable,
                      "threads": os.environ.get("OMP_NUM_THREADS", "unset")},
-            "all_cores": {"value": workers / (20 * all_wall), "unit": "GE solves/s", "cores": workers,
-                          "kind": "port",
-                          "sample": f"{workers} Table II cells, one near-root K_s evaluation each (r* - 0.03 %), one "
-                                    f"process per core: {all_wall:.2f} s wall (per cell {min(x[0] for x in res):.2f}-"
-                                    f"{max(x[0] for x in res):.2f} s); GE solves/s = cells / (20 x wall)"}}
+            "all_cores": {"value": workers / all_wall, "unit": "GE solves/s", "cores": workers, "kind": "port",
+                          "sample": (f"{workers} processes, each one complete oracle GE solve of the same cell at "
+                                     f"once: {all_wall:.1f} s wall (per solve {min(x[0] for x in res):.1f}-"
+                                     f"{max(x[0] for x in res):.1f} s); {workers} = the GPU box's CPU share per GPU "
+                                     f"(nproc {n_cpu})")},
+            "ks_reference": ks}
 
 
 def main():
@@ -506,14 +647,17 @@ def main():
     ap.add_argument("--c1-steps", type=int, default=1)
     ap.add_argument("--c3-agents", type=int, default=N_AGENTS_C3)
     ap.add_argument("--c3-periods", type=int, default=T_C3)
-    ap.add_argument("--legs", default="table2,configs1,configs3,table2_reference")
+    ap.add_argument("--stress-grid", type=int, default=STRESS_N_A)
+    ap.add_argument("--legs", default="table2,configs1,configs3,configs4,table2_reference")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: one-GPU rehearsal of the multi-rank run (every rank on device 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
 
     import torch
-    world, rank, local = setup_dist()
+    world, rank, local = setup_dist(args.dist_backend)
     if args.gpus != world:
         log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting n_gpus={world}")
     dev = torch.device("cuda", local)
@@ -523,6 +667,7 @@ def main():
     barrier(world)
     legs = set(args.legs.split(","))
     t2 = table2_leg(args, world, rank, dev)
+    sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]
     line = {
         "metric": "GE solves/sec (Table II sweep); agent-periods/sec; % HBM roofline",
         "value": t2["value"],
@@ -540,7 +685,7 @@ def main():
                                f"Aiyagari GE in r (Brent on K_s = K_d), {args.grid}-pt asset grid, 7-state Tauchen, "
                                "Young-lottery stationary distribution; one step = the whole sweep",
                    "calibrations": N_TABLE2, "n_a": args.grid, "S": 7,
-                   "parallelism": f"calibrations split round-robin over {world} GPU(s), no data-path collective; "
+                   "parallelism": f"calibrations split round-robin over {world} rank(s), no data-path collective; "
                                   "per GPU 3 independent root searches (own handle, stream, host thread)"},
         "roofline": {"kernel": "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery "
                                "stationary distribution)", "bound": "hbm",
@@ -553,21 +698,30 @@ def main():
                      "launch": "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
                                "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
                                "updates)",
-                     "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"])},
+                     "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"]),
+                     # concurrent launches (independent groups) overlap: the device-level rate is the
+                     # algorithmic bytes of a whole sweep over the sweep's wall time
+                     "device_aggregate": {"achieved": sweep_bytes / t2["seconds_per_sweep"] / 1e9,
+                                          "frac": sweep_bytes / t2["seconds_per_sweep"] / 1e9 / HBM_PEAK_GBS,
+                                          "note": "algorithmic bytes of all launches of a sweep / sweep wall time"}},
         "table2": {k: t2[k] for k in ("seconds_per_sweep", "evaluations_rank0", "hist_launches_per_sweep",
                                       "hist_kernel_ms_per_sweep", "r_percent", "saving_rate_percent")},
         "cpu_baseline": None,
     }
-    if "configs1" in legs or "configs3" in legs:
-        c1, econ, agent = configs1_leg(args, world, rank, dev)
-        if "configs1" in legs:
-            line["configs1"] = c1
-        if "configs3" in legs:
-            line["configs3"] = configs3_leg(args, world, rank, dev, econ, agent)
+    if args.dist_backend == "gloo" and world > 1:
+        line["rehearsal"] = f"{world} ranks on one GPU (gloo rendezvous and collectives)"
+    if "configs1" in legs:
+        line["configs1"] = configs1_leg(args, world, rank, dev)[0]
+    if "configs3" in legs:
+        line["configs3"] = configs3_leg(args, world, rank, dev)
+    if "configs4" in legs:
+        line["configs4"] = configs4_leg(args, world, rank, dev)
     if "table2_reference" in legs:
         line["table2_reference"] = table2_reference_leg(world, rank, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.grid, [x / 100.0 for x in t2["r_percent"]])
+        ks_iters = line.get("table2_reference", {}).get("ge_iterations_rank0")
+        line["cpu_baseline"] = cpu_baseline(args.grid, t2["r_percent"][N_TABLE2_CPU_CELL] / 100.0,
+                                            ks_ge_iterations=ks_iters)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -341,6 +341,13 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     BiCGSTAB from the given mass (hist_krylov.hip; stops at a mass
                                     T x with max|T x - x| < tol, the plain iteration's rule; counts
                                     are matvecs); takes precedence over AIY_OPT_HIST_ACCEL */
+#define AIY_OPT_GE_RESIDENT 10    /* value != 0 (default): aiy_ge_stationary runs the whole search of
+                                    every calibration in ONE device-resident launch (each
+                                    calibration's cluster: EGM cycles, lottery, BiCGSTAB, K_s and the
+                                    root search on device, ge_resident.hip) when accel < 0, S <= 8
+                                    and every cluster fits the device at once; else the host loop */
+#define AIY_OPT_CU_LIMIT 11       /* compute units the resident launches of this handle may fill
+                                    (0: the device's; several processes sharing one GPU: a share) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
@@ -412,6 +419,10 @@ typedef struct {
                             their last change by lambda / (1 - lambda) at chunk boundaries
                             where the cycle distances fall at a steady rate lambda (egm.hip;
                             the stopping rule is unchanged)                                   */
+  int32_t* status_out;   /* HOST [n_cal] or NULL: per calibration, bit 1 = some evaluation's
+                            household solve stopped at max_egm_cycles above its tolerance,
+                            bit 2 = some distribution solve stopped at max_hist_iter, bit 4 =
+                            the search stopped at max_steps before r_tol (0: converged)      */
 } aiy_ge_options;
 
 /* Device scratch the call needs (caller-owned `work`), -1 for bad sizes. */
@@ -428,6 +439,17 @@ int64_t aiy_ge_stationary_work_bytes(int32_t n_cal, int32_t S, int32_t n_a);
 int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* model, const aiy_ge_options* opt,
                           void* work, double* r_out, double* K_out, double* Ks_out, int32_t* steps_out,
                           int32_t* egm_cycles_out, int32_t* hist_iters_out, aiy_stream stream);
+
+/* Plan of the device-resident GE search for (n_cal, S, n_a): returns 1 and out4 =
+ * {workgroups per calibration cluster, asset columns per workgroup, columns per thread,
+ * blocks of the launch} when aiy_ge_stationary would run it, else 0.  Host-only. */
+int32_t aiy_ge_resident_plan(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_a, int32_t* out4);
+
+/* Device-resident GE launch statistics (measurement hook): kernel milliseconds (HIP events
+ * around each launch on its stream), launches, (state, node) point-matvecs of the
+ * distribution solves and EGM cycles inside them, since the last reset.  Host-only. */
+int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, double* point_matvecs,
+                            double* egm_cycles, int32_t reset);
 
 /* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
  * the device-resident distribution-iteration launches since the last reset (HIP events on

@@ -71,8 +71,10 @@ def prices(r, alpha, delta):
 # --------------------------------------------------------------------------------------
 # E1 (inner): stationary EGM
 # --------------------------------------------------------------------------------------
-def egm_step(m_next, c_next, beta, rho, aGrid, R, w, lab, P):
-    """Stationary solve_Aiyagari step.  Tables [S][n_a + 1]; m_next None = terminal c = m."""
+def egm_step(m_next, c_next, beta, rho, aGrid, R, w, lab, P, matmul=False):
+    """Stationary solve_Aiyagari step.  Tables [S][n_a + 1]; m_next None = terminal c = m.
+    matmul=True forms the expectation as one BLAS product V @ P.T (same sums, another
+    summation order; used for the large fixtures, tests/golden/make_golden_fullsize.py)."""
     S = P.shape[0]
     nA = aGrid.size
     mN = R * aGrid[:, None] + w * lab[None, :]             # [a, s']
@@ -90,7 +92,7 @@ def egm_step(m_next, c_next, beta, rho, aGrid, R, w, lab, P):
                 c[q < x[0]] = np.nan
             vP[:, sp] = c ** -rho
         V = R * vP
-        E = beta * np.sum(V[:, None, :] * P[None, :, :], axis=2)
+        E = beta * (V @ P.T if matmul else np.sum(V[:, None, :] * P[None, :, :], axis=2))
         cNow = E ** (-1.0 / rho)
     mNow = aGrid[:, None] + cNow
     m_out = np.empty((S, nA + 1))
@@ -102,13 +104,13 @@ def egm_step(m_next, c_next, beta, rho, aGrid, R, w, lab, P):
     return m_out, c_out
 
 
-def egm_solve(beta, rho, aGrid, R, w, lab, P, tol=1e-6, max_cycles=5000):
+def egm_solve(beta, rho, aGrid, R, w, lab, P, tol=1e-6, max_cycles=5000, matmul=False):
     """HARK-style infinite-horizon loop (cold start, sup-norm over m and c, stop when
     dist <= tol)."""
-    m, c = egm_step(None, None, beta, rho, aGrid, R, w, lab, P)
+    m, c = egm_step(None, None, beta, rho, aGrid, R, w, lab, P, matmul)
     cycles = 1
     while True:
-        m2, c2 = egm_step(m, c, beta, rho, aGrid, R, w, lab, P)
+        m2, c2 = egm_step(m, c, beta, rho, aGrid, R, w, lab, P, matmul)
         with np.errstate(invalid="ignore"):
             dist = max(np.max(np.abs(m2 - m)), np.max(np.abs(c2 - c)))
         go = dist > tol and cycles < max_cycles
@@ -183,10 +185,10 @@ def stationary_hist(lo, wlo, P, nA, tol=1e-12, max_iter=100000, mass0=None, step
 # --------------------------------------------------------------------------------------
 # E1 (outer): GE bisection on r
 # --------------------------------------------------------------------------------------
-def capital_supply(r, cal, aGrid, lab, P, egm_tol=1e-8, hist_tol=1e-12, fast=False):
+def capital_supply(r, cal, aGrid, lab, P, egm_tol=1e-8, hist_tol=1e-12, fast=False, egm_matmul=False):
     w, _ = prices(r, cal["CapShare"], cal["DeprFac"])
     R = 1.0 + r
-    m, c, cycles, _ = egm_solve(cal["DiscFac"], cal["CRRA"], aGrid, R, w, lab, P, tol=egm_tol)
+    m, c, cycles, _ = egm_solve(cal["DiscFac"], cal["CRRA"], aGrid, R, w, lab, P, tol=egm_tol, matmul=egm_matmul)
     lo, wlo, _ = savings_lottery(m, c, aGrid, R, w, lab)
     mass, iters, _ = stationary_hist(lo, wlo, P, aGrid.size, tol=hist_tol, step=hist_step_fast if fast else None)
     K = float(np.sum(mass * aGrid[None, :]))
@@ -194,7 +196,8 @@ def capital_supply(r, cal, aGrid, lab, P, egm_tol=1e-8, hist_tol=1e-12, fast=Fal
 
 
 def ge_bisect(cal, aGrid, lab, P, r_lo=None, r_hi=None, r_tol=1e-7, max_iter=60, **kw):
-    """Bisection on r for K_s(r) = K_d(r).  Returns dict(r, K, KtoY, saving_rate, iters)."""
+    """Bisection on r for K_s(r) = K_d(r).  Returns dict(r, K, KtoY, saving_rate, iters,
+    lo, hi) -- (lo, hi) the final bracket, r its midpoint."""
     a, d, b = cal["CapShare"], cal["DeprFac"], cal["DiscFac"]
     lo = -d * 0.5 if r_lo is None else r_lo
     hi = 1.0 / b - 1.0 - 1e-9 if r_hi is None else r_hi
@@ -211,7 +214,7 @@ def ge_bisect(cal, aGrid, lab, P, r_lo=None, r_hi=None, r_tol=1e-7, max_iter=60,
     r = 0.5 * (lo + hi)
     _, K = prices(r, a, d)
     KtoY = K ** (1.0 - a)
-    return dict(r=r, K=K, KtoY=KtoY, saving_rate=d * KtoY, iters=it)
+    return dict(r=r, K=K, KtoY=KtoY, saving_rate=d * KtoY, iters=it, lo=lo, hi=hi)
 
 
 def make_stationary_grid(aMin=0.001, aMax=50.0, aCount=32, aNestFac=2):

@@ -1,0 +1,233 @@
+"""GPU parity at the sizes the bench numbers are quoted on, against
+full-size fixtures made by the CPU oracle (tests/golden/make_golden_fullsize.py,
+tests/golden/make_golden_c3.py):
+
+* configs[2] -- the bench's own Table II sweep (solve_table2(method="brent"): 3 independent
+  groups, secant starts, loose bracketing, EGM extrapolation, BiCGSTAB distribution) at
+  N_a = 10 000 against the oracle's ge_bisect of all 24 cells (cold EGM to 1e-8, cold Young
+  histogram to 1e-12, bisection to 1e-7): r within R_TOL, K/Y within KY_RTOL relative;
+* configs[4] -- the 3 stress cells (25-state Rouwenhorst, N_a = 50 000) the same way, and
+  K_s at the oracle's root through the 98-workgroup, v-in-HBM BiCGSTAB kernel and through
+  the plain device iteration;
+* configs[3] -- the bench's 99 999 998-agent panel (HBM-streaming persistent kernel, and the
+  two-step sharded period with the all-reduce between the library's steps) for the first
+  periods, against the oracle's history of the same population (labour counts exact, K / M
+  history to 1e-12);
+* the multi-rank bench rehearsed on one GPU (2 ranks, gloo): the same r and K history as
+  one rank.
+
+Tolerances: north_star asks r and K/Y within 1e-5; both solvers stop within r_tol = 1e-7
+of their own root, whose positions differ by the EGM / histogram stopping rules (egm 1e-8,
+hist 1e-12), so the tests hold r to R_TOL = 5e-7.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+R_TOL = 5e-7          # |r_device - r_oracle| (north_star: 1e-5)
+KY_RTOL = 5e-6        # K/Y relative (K/Y = (alpha / (r + delta))^((1-alpha)/(1-alpha)) moves ~4 dr / (r + delta))
+
+
+def _fixture(name):
+    return json.load(open(os.path.join(GOLD, f"fullsize_{name}.json")))
+
+
+def _stationary_cal(c):
+    from aiyagari_hark_amd.stationary import Calibration
+    return Calibration(LaborAR=c["rho"], LaborSD=c["sigma"], CRRA=c["crra"], LaborStatesNo=c["S"], income=c["income"])
+
+
+@pytest.mark.timeout(300)
+def test_table2_bench_sweep_matches_oracle_fullsize(gpu):
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    fx = _fixture("table2")
+    cells = fx["cells"]
+    cals = table2_calibrations()
+    assert len(cells) == len(cals) == 24
+    for c, cal in zip(cells, cals):   # same order, same calibrations
+        assert (c["rho"], c["sigma"], c["crra"]) == (cal.LaborAR, cal.LaborSD, cal.CRRA)
+    res = solve_table2(cals, n_a=10_000, device=gpu, method="brent")   # the bench's call (bench.py table2_leg)
+    r_o = np.array([c["r"] for c in cells])
+    ky_o = np.array([c["KtoY"] for c in cells])
+    dr = np.abs(res.r - r_o)
+    print(f"\nTable II at N_a = 10 000: max |r - r_oracle| = {dr.max():.2e} (cell {int(dr.argmax())}), "
+          f"max rel K/Y {np.max(np.abs(res.KtoY - ky_o) / ky_o):.2e}")
+    assert np.all(res.status == 0), res.status
+    assert np.all(dr <= R_TOL), dr
+    assert np.all(np.abs(res.KtoY - ky_o) / ky_o <= KY_RTOL)
+    # every oracle root is bracketed to 1e-7 and the device root lies within R_TOL of it
+    assert all(c["hi"] - c["lo"] <= 1e-7 for c in cells)
+
+
+def test_solve_table2_default_device(gpu):
+    """solve_table2 with device=None (documented in INTEGRATION.md)
+    takes the current device, also on the grouped path."""
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    cals = table2_calibrations()[:3]
+    res = solve_table2(cals, n_a=400, method="brent")
+    ref = solve_table2(cals, n_a=400, method="brent", device=gpu)
+    assert np.array_equal(res.r, ref.r)
+
+
+@pytest.mark.timeout(600)
+def test_stress_ge_matches_oracle_fullsize(gpu):
+    from aiyagari_hark_amd.stationary import solve_table2
+    fx = _fixture("stress")
+    cells = fx["cells"]
+    cals = [_stationary_cal(c) for c in cells]
+    res = solve_table2(cals, n_a=cells[0]["n_a"], device=gpu, method="brent")   # bench.py configs4_leg
+    r_o = np.array([c["r"] for c in cells])
+    dr = np.abs(res.r - r_o)
+    print(f"\nstress (25 states, N_a = 50 000): |r - r_oracle| = {dr}")
+    assert np.all(res.status == 0), res.status
+    assert np.all(dr <= R_TOL), dr
+
+
+@pytest.mark.timeout(600)
+def test_stress_capital_supply_at_oracle_root(gpu):
+    """K_s(r) at the oracle's root, cold, on the bench's kernels: BiCGSTAB (25 states: one
+    column per thread, v in HBM, 98 workgroups per calibration) and the plain resident
+    iteration (the oracle's arithmetic) against the oracle's K_s."""
+    from aiyagari_hark_amd import setup_math as sm
+    from aiyagari_hark_amd.stationary import StationaryBatch
+    fx = _fixture("stress")
+    cells = fx["cells"]
+    n_a = cells[0]["n_a"]
+    b = StationaryBatch([_stationary_cal(c) for c in cells], sm.make_grid_exp_mult(0.001, 50.0, n_a, 2), device=gpu)
+    r = np.array([c["r"] for c in cells])
+    K_bicg, _, it_b = b.capital_supply(r, egm_tol=1e-8, hist_tol=1e-12, accel=-1)
+    K_plain, _, it_p = b.capital_supply(r, egm_tol=1e-8, hist_tol=1e-12, accel=0)
+    K_o = np.array([c["Ks_at_r"] for c in cells])
+    print(f"\nK_s at the oracle root: oracle {K_o}, BiCGSTAB {K_bicg} ({it_b} matvecs), plain {K_plain} ({it_p} iters);"
+          f" oracle iterations {[c['hist_iters_at_r'] for c in cells]}")
+    assert np.all(np.abs(K_plain - K_o) / K_o < 1e-6)
+    assert np.all(np.abs(K_bicg - K_o) / K_o < 1e-6)
+    assert np.all(np.abs(K_bicg - K_plain) / K_plain < 1e-5)
+
+
+# ---------------------------------------------------------------------------------------
+# configs[3]: the 1e8-agent panel
+# ---------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c3(gpu):
+    import bench
+    fx = _fixture_c3()
+    econ, agent = bench.c3_policy(gpu, fx["n_a"])
+    c_tab = agent.solution[0].c_tab.cpu().numpy()
+    return fx, econ, agent, hashlib.sha256(np.ascontiguousarray(c_tab).tobytes()).hexdigest()
+
+
+def _fixture_c3():
+    return json.load(open(os.path.join(GOLD, "fullsize_c3.json")))
+
+
+def _check_c3(fx, hA, hM, lab_counts, a_sample, lab_sample, T):
+    assert np.max(np.abs(np.asarray(hA[:T]) - fx["hist_A"][:T]) / np.asarray(fx["hist_A"][:T])) < 1e-12
+    assert np.max(np.abs(np.asarray(hM[:T]) - fx["hist_M"][:T]) / np.asarray(fx["hist_M"][:T])) < 1e-12
+    if lab_counts is not None:
+        assert [int(x) for x in lab_counts] == fx["lab_counts"][T - 1]
+    if a_sample is not None:
+        assert np.array_equal(lab_sample, fx["sample_lab"])
+        assert np.max(np.abs(a_sample - fx["sample_a"])) / np.max(np.abs(fx["sample_a"])) < 1e-12
+
+
+def test_configs3_policy_is_the_oracle_policy(c3):
+    """The converged 10 000-point KS-form household the configs[3] bench leg simulates is
+    bit-identical to the oracle's (same cycle count; CRRA 1 EGM steps are bit-exact)."""
+    fx, econ, agent, sha = c3
+    assert agent.completed_cycles + 1 == fx["egm_cycles"]
+    assert sha == fx["policy_sha256"]
+
+
+@pytest.mark.timeout(300)
+def test_configs3_fullsize_streaming_panel_matches_oracle(c3, gpu):
+    """bench.py configs3_leg's panel (one rank: the HBM-streaming persistent kernel) over
+    the fixture's periods: labour counts of all 99 999 998 agents exact, K / M history and
+    sampled agents to 1e-12."""
+    import bench
+    fx, econ, agent, _ = c3
+    T = fx["periods"]
+    p, reset = bench.c3_panel(gpu, econ, agent, fx["agents"], T)
+    p.run(0, T, shock_mode="philox", seed=fx["seed"], ge_iter=fx["ge_iter"])
+    torch.cuda.synchronize()
+    idx = torch.as_tensor(fx["sample_idx"], device=gpu)
+    counts = torch.bincount(p.lab.long(), minlength=7).cpu().numpy()
+    _check_c3(fx, p.hist_A.cpu().numpy(), p.hist_M.cpu().numpy(), counts, p.a[idx].cpu().numpy(),
+              p.lab[idx].cpu().numpy(), T)
+    a = p.a.cpu().numpy()
+    assert abs(float(np.sum(a)) - fx["a_sum_final"]) / fx["a_sum_final"] < 1e-12
+
+
+@pytest.mark.timeout(300)
+def test_configs3_fullsize_two_step_shards_match_oracle(c3, gpu):
+    """The sharded form of configs[3] at full size: two contiguous shards (the second
+    starts at an even global index, 49 999 999), each period aiy_sim_period_local on both
+    -> the caller's sum -> aiy_sim_period_prices, against the oracle's history."""
+    import ctypes
+
+    import bench
+    from aiyagari_hark_amd import _lib
+    fx, econ, agent, _ = c3
+    T, N = fx["periods"], fx["agents"]
+    shards = [bench.c3_panel(gpu, econ, agent, N, T, 2, r)[0] for r in range(2)]
+    h = _lib.handle(gpu.index)
+    sp = _lib.stream_ptr()
+    for t in range(T):
+        for p in shards:
+            pm = p._model[0]
+            h.check(h.lib.aiy_sim_period_local(h.h, ctypes.byref(pm), p.n_local, p.agent_offset, _lib.ptr(p.a),
+                                               _lib.ptr(p.lab), None, None, fx["seed"], fx["ge_iter"], t,
+                                               _lib.ptr(p.sow), sp), "local")
+        total = shards[0].sow[6] + shards[1].sow[6]
+        for p in shards:
+            p.sow[6] = total
+            pm, mk = p._model[0], p._model[1]
+            h.check(h.lib.aiy_sim_period_prices(h.h, ctypes.byref(pm), ctypes.byref(mk), N, t, _lib.ptr(p.sow),
+                                                _lib.ptr(p.hist_A), _lib.ptr(p.hist_M), sp), "prices")
+    torch.cuda.synchronize()
+    counts = sum(torch.bincount(p.lab.long(), minlength=7).cpu().numpy() for p in shards)
+    _check_c3(fx, shards[1].hist_A.cpu().numpy(), shards[1].hist_M.cpu().numpy(), counts, None, None, T)
+    assert np.array_equal(shards[0].hist_A[:T].cpu().numpy(), shards[1].hist_A[:T].cpu().numpy())
+
+
+# ---------------------------------------------------------------------------------------
+# the multi-rank bench, rehearsed on one GPU
+# ---------------------------------------------------------------------------------------
+def _bench_line(extra, timeout):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+           "--legs", "table2,configs3", "--grid", "2000", "--c3-agents", "2100000", "--c3-periods", "40"] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    sys.stderr.write(out.stderr[-3000:])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(400)
+def test_bench_two_rank_rehearsal_matches_one_rank(gpu):
+    """bench.py --gpus 2 --dist-backend gloo: two rank processes on device 0 (the
+    driver's 8-GPU run rehearsed): Table II cells split round-robin, configs[3] agents
+    sharded with the per-period sum through the two-step period; the same r as one rank
+    and the same K history to 1e-12 (summation order of the shard sums)."""
+    one = _bench_line([], 180)
+    two = _bench_line(["--gpus", "2", "--dist-backend", "gloo"], 300)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert "rehearsal" in two
+    # the per-calibration searches do not depend on the split (same cluster size per cell);
+    # r_percent is rounded to 1e-6 percentage points
+    assert np.max(np.abs(np.array(two["table2"]["r_percent"]) - one["table2"]["r_percent"])) <= 2e-6
+    k1, k2 = np.array(one["configs3"]["K_first"]), np.array(two["configs3"]["K_first"])
+    assert np.max(np.abs(k1 - k2) / k1) < 1e-12
+    assert abs(one["configs3"]["K_final"] - two["configs3"]["K_final"]) / one["configs3"]["K_final"] < 1e-12
