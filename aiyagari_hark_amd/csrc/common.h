@@ -24,14 +24,24 @@ constexpr double kBorrowNode = 0.0000001;  // Aiyagari_Support.py:1503-1504
 // atomics and stores of the previous kernels: measured on MI355X, a solve whose
 // convergence slot was read with s_load kept iterating ~20 cycles past convergence.
 // ---------------------------------------------------------------------------------
+// Every control word and hand-off buffer lives in global memory (hipMalloc): the accesses
+// are typed global so they compile to global_load/store ... sc1 even where the compiler
+// cannot prove the address space of a generic pointer (a flat_ access is slower and is not
+// a valid stand-in for the agent-scope acquire, MI355X_MICROARCH.md hand-off rules).
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr<T> to_global(T* p) {
+  return (gptr<T>)p;
+}
 __device__ __forceinline__ unsigned long long load_u64_agent(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(to_global(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double load_f64_agent(const double* p) {
   return __longlong_as_double((long long)load_u64_agent(reinterpret_cast<const unsigned long long*>(p)));
 }
 __device__ __forceinline__ void store_u64_agent(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(to_global(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void store_f64_agent(double* p, double v) {
   store_u64_agent(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));

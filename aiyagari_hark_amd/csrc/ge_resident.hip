@@ -84,7 +84,11 @@ struct GeRun {
   int* out_cyc;
   int* out_its;
   int* out_status;
+  double* out_prof;       // [n_cal][kGeProf] workgroup 0's phase times (us) and counts
 };
+// per-calibration profile of the launch (workgroup 0, s_memrealtime at 100 MHz): EGM, lottery,
+// distribution solve, K reduction + search, whole search (us); EGM cycles, matvecs, evaluations
+constexpr int kGeProf = 8;
 
 // Search state of one calibration, one copy per workgroup (thread 0 writes, all read).
 struct GeState {
@@ -93,6 +97,7 @@ struct GeState {
   int steps, loose, refine, warm_egm, secant, fresh_mass, status, n, stop, nan_stop, moved, extrap;
   int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
   long long cyc_sum, its_sum;
+  unsigned long long t_egm, t_lot, t_hist, t_k, t0;
   unsigned nc_prev[2];
   unsigned nbc;            // counting barriers passed
 };
@@ -121,8 +126,8 @@ __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w
     for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
     const unsigned long long b = (unsigned long long)__double_as_longlong(x);
     unsigned long long* g = slot + (size_t)w * kHcRedRec + 2 * v;
-    __hip_atomic_store(g, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 1, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (wid == 0) {
     double xa[kHkRed], xb[kHkRed];
@@ -138,8 +143,8 @@ __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w
           double x = 0.0;
           if (v < nv && w2 < G) {
             const unsigned long long* g = slot + (size_t)w2 * kHcRedRec + 2 * v;
-            const unsigned long long hi = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long lo = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long hi = __hip_atomic_load(to_global(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long lo = __hip_atomic_load(to_global(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
             x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
           }
@@ -150,7 +155,7 @@ __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(to_global(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     } while (true);
@@ -173,11 +178,11 @@ __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w
 // hist_bicg.h column of the same thread): for every row s of `src` (S rows of n_a + 1
 // nodes) the HARK LinearInterp at q = R a_j + Wl[s], by the window search of egm.hip over
 // agent-scope loads; sink(tile, lane column, s, q, value) takes the result.
-template <int SMAX, typename Sink>
+template <int SMAX, typename Sink, typename Begin, typename End>
 __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, const double* __restrict__ a_grid,
                                              const double* __restrict__ src_m, const double* __restrict__ src_c,
                                              double R, const double* s_Wl, int* s_hint, double* lds_win,
-                                             Sink&& sink) {
+                                             Sink&& sink, Begin&& begin, End&& end) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int n = n_a, n1 = n_a + 1;
@@ -192,6 +197,7 @@ __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, con
     const int j = jr < j1 ? jr : j1 - 1;   // lanes past the range repeat the last column
     const double a = a_grid[j];
     int* hint = s_hint + tile * SMAX;
+    begin(tile, j);
     auto fetch = [&](int r, RowWin& wn) {
       const int rr = r < S ? r : S - 1;
       load_win<true>(src_m + (size_t)rr * n1, src_c + (size_t)rr * n1, n, win_base(hint[rr], n1), lane, wn);
@@ -244,6 +250,7 @@ __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, con
       hint[s] = __builtin_amdgcn_readfirstlane(lb);
       sink(tile, jr, j, s, q, f);
     }
+    end(tile, j, a);
   }
 }
 
@@ -286,66 +293,115 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
     }
     return 0.0;
   }
-  // tiles one after another per wave: V of a tile's rows (phase 1), then its outputs
-  int cur_tile = -1;
-  auto flush = [&](int tile) {   // phase 2 of `tile` (its V complete; each lane reads its own)
-    const int jr = j0 + tile * kTile + lane;
-    const int j = jr < j1 ? jr : j1 - 1;
-    const double a = a_grid[j];
-    for (int s = 0; s < S; ++s) {
-      double pm = 0.0, pc = 0.0;
-      if (track) {
-        pm = load_f64_agent(&src_m[(size_t)s * n1 + j + 1]);
-        pc = load_f64_agent(&src_c[(size_t)s * n1 + j + 1]);
-      }
-      double sum;
-      if constexpr (SC > 0) sum = pairwise_dot<SC>(Vw + lane, s_Pe + s * SC);
-      else sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vw[t * kTile + lane] * uniform_f64(s_Pe[s * S + t]); });
-      const double E = beta * sum;                     // EndOfPrdvP (AS:1485)
-      const double c = inv_marg<PK>(E, gam);           // AS:1490
-      const double m = a + c;                          // AS:1499
-      store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], m);
-      store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
-      if (track) dmax = nan_max(dmax, nan_max(fabs(m - pm), fabs(c - pc)));
-      if (j == 0) {   // the (1e-7, 1e-7) node (AS:1503-1504)
-        store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
-        store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
+  // tiles one after another per wave: the previous tables' values at the lane's node
+  // (distance) in flight from the tile's start, V of the tile's rows (phase 1), then its
+  // outputs (phase 2)
+  constexpr int NP = SC > 0 ? SC : SMAX;
+  double pmv[NP], pcv[NP];
+  auto begin = [&](int, int j) {
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      pmv[s] = 0.0;
+      pcv[s] = 0.0;
+      if (track && s < S) {
+        pmv[s] = load_f64_agent(&src_m[(size_t)s * n1 + j + 1]);
+        pcv[s] = load_f64_agent(&src_c[(size_t)s * n1 + j + 1]);
       }
     }
   };
-  // the window pass visits a tile's rows in order, the redo rows after them: the tile's V
-  // is complete when the pass moves to the next tile (or ends)
+  auto end = [&](int, int j, double a) {   // phase 2 (each lane reads its own V)
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      if (s < S) {
+        __builtin_amdgcn_sched_barrier(0);   // one state's P reads at a time (no hoisting of all S x S)
+        double sum;
+        if constexpr (SC > 0) sum = pairwise_dot<SC>(Vw + lane, s_Pe + s * SC);
+        else sum = np_pairwise_sum<SMAX>(S, [&](int t) { return Vw[t * kTile + lane] * uniform_f64(s_Pe[s * S + t]); });
+        const double E = beta * sum;                     // EndOfPrdvP (AS:1485)
+        const double c = inv_marg<PK>(E, gam);           // AS:1490
+        const double m = a + c;                          // AS:1499
+        store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], m);
+        store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
+        if (track) dmax = nan_max(dmax, nan_max(fabs(m - pmv[s]), fabs(c - pcv[s])));
+        if (j == 0) {   // the (1e-7, 1e-7) node (AS:1503-1504)
+          store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
+          store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
+        }
+      }
+    }
+  };
   ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, src_m, src_c, R, s_Wl, s_hint, lds_win,
-                     [&](int tile, int, int, int sp, double, double f) {
-                       if (tile != cur_tile) {
-                         if (cur_tile >= 0) flush(cur_tile);
-                         cur_tile = tile;
-                       }
+                     [&](int, int, int, int sp, double, double f) {
                        Vw[sp * kTile + lane] = R * marg_u<PK>(f, gam);   // RnextArray * MargValueFuncCRRA
-                     });
-  if (cur_tile >= 0) flush(cur_tile);
+                     },
+                     begin, end);
   return dmax;
+}
+
+// The kernel's LDS at file scope, so the search loop, the EGM cycle and the lottery (their
+// own non-inlined functions, each with its own register allocation) address it directly.
+constexpr int kGeSmax = 8;
+extern __shared__ double ge_dyn[];                 // histogram: span buffer + v; EGM: V tiles + windows
+__shared__ double ge_s_part[kHkRed][kGeWaves];
+__shared__ double ge_s_res[kHkRed];
+__shared__ int ge_s_flag;
+__shared__ double ge_s_Pe[kGeSmax * kGeSmax];     // P[s][s'] unpadded (egm_phase2's layout)
+__shared__ double ge_s_Wl[kGeSmax];               // w l(s')
+__shared__ int ge_s_hint[kGeMaxTiles * kGeSmax];  // window hints per (tile, row)
+__shared__ unsigned ge_s_nc;
+__shared__ GeState ge_st;
+
+template <int SMAX, int SC, int PK>
+__device__ __forceinline__ double ge_egm_cycle_fn(int S, int n_a, int j0, int j1, const double* a_grid,
+                                               const double* src_m, const double* src_c, double* dst_m,
+                                               double* dst_c, bool track, double R, double beta, double gam) {
+  return ge_egm_cycle<SMAX, SC, PK>(S, n_a, j0, j1, a_grid, src_m, src_c, dst_m, dst_c, track, R, beta, gam, ge_s_Wl,
+                                    ge_s_Pe, ge_s_hint, ge_dyn, ge_dyn + (size_t)kGeWaves * SMAX * kTile);
+}
+
+// lottery of the own columns on the final tables (hist.hip hist_lottery_kernel's arithmetic)
+template <int SMAX>
+__device__ __forceinline__ void ge_lottery_fn(int S, int n_a, int j0, int j1, const double* a_grid, const double* fm,
+                                           const double* fc, double R, bool have_prev, int* LO, double* WL) {
+  ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, fm, fc, R, ge_s_Wl, ge_s_hint, ge_dyn + (size_t)kGeWaves * SMAX * kTile,
+                     [&](int, int jr, int, int s, double q, double c) {
+                       if (jr >= j1) return;
+                       const double ap = q - c;
+                       const size_t o = (size_t)s * n_a + jr;
+                       int d = -1;
+                       if (have_prev) {   // last evaluation's bracket as the first guess
+                         const int h = LO[o];
+                         if (h >= 0 && h < n_a - 1 && a_grid[h] <= ap && ap < a_grid[h + 1]) d = h;
+                       }
+                       if (d < 0) {       // searchsorted(a_grid, a', 'right') - 1
+                         int lo = 0, hi = n_a;
+                         while (lo < hi) {
+                           const int mid = lo + ((hi - lo) >> 1);
+                           if (a_grid[mid] <= ap) lo = mid + 1; else hi = mid;
+                         }
+                         d = lo - 1;
+                       }
+                       d = d < 0 ? 0 : (d > n_a - 2 ? n_a - 2 : d);
+                       double wl = (a_grid[d + 1] - ap) / (a_grid[d + 1] - a_grid[d]);
+                       wl = wl < 0.0 ? 0.0 : (wl > 1.0 ? 1.0 : wl);
+                       LO[o] = d;
+                       WL[o] = wl;
+                     },
+                     [](int, int) {}, [](int, int, double) {});
 }
 
 template <int SMAX, int SC, int KC>
 __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
   constexpr int TH = kGeTH;
-  extern __shared__ double dyn[];   // histogram: span buffer + v; EGM: V tiles + windows (aliased)
-  __shared__ int s_base[SMAX];
-  __shared__ int s_pub[2 * SMAX][2];
-  __shared__ int s_tot;
-  __shared__ HcCand s_cand[SMAX][kHcCand];
-  __shared__ int s_ncand[SMAX];
-  __shared__ unsigned short s_cinfo[KC * SMAX * TH];
-  __shared__ double s_P[SMAX * SMAX];
-  __shared__ double s_part[kHkRed][TH / kWave];
-  __shared__ double s_res[kHkRed];
-  __shared__ int s_flag, s_stop;
-  __shared__ double s_Pe[SMAX * SMAX];   // P[s][s'] unpadded (egm_phase2's layout)
-  __shared__ double s_Wl[SMAX];          // w l(s')
-  __shared__ int s_hint[kGeMaxTiles * SMAX];
-  __shared__ unsigned s_nc;
-  __shared__ GeState st;
+  static_assert(SMAX <= kGeSmax, "file-scope LDS sized for 8 states");
+  GeState& st = ge_st;
+  double (*s_part)[TH / kWave] = ge_s_part;
+  double* s_res = ge_s_res;
+  int& s_flag = ge_s_flag;
+  double* s_Pe = ge_s_Pe;
+  double* s_Wl = ge_s_Wl;
+  int* s_hint = ge_s_hint;
+  unsigned& s_nc = ge_s_nc;
 
   const int per = gridDim.x >> 3;
   const int u = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-contiguous work order
@@ -372,10 +428,6 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
   unsigned nb = 0, ne = 0;   // plain barriers / reductions passed (hk_solve counts on)
   const int pk = gam == 1.0 ? 1 : (gam == 3.0 ? 3 : (gam == 5.0 ? 5 : 0));
 
-  const HkShared<SMAX, KC, TH> L{dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop};
-  double* lds_v = dyn;
-  double* lds_win = dyn + (size_t)kGeWaves * SMAX * kTile;
 
   for (int q = tid; q < S * S; q += TH) s_Pe[q] = g.P[(size_t)cal * S * S + q];
   for (int q = tid; q < kGeMaxTiles * SMAX; q += TH) s_hint[q] = -1;
@@ -390,6 +442,8 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     st.nc_prev[0] = st.nc_prev[1] = 0u;
     st.nbc = 0u;
     for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
+    st.t_egm = st.t_lot = st.t_hist = st.t_k = 0ull;
+    st.t0 = __builtin_amdgcn_s_memrealtime();
   }
   __syncthreads();
   auto plain_barrier = [&]() -> bool {
@@ -445,6 +499,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     }
     // ---- the household solve ([HARK] solve_agent: cycles until the sup-norm change of the
     //      tables is <= tol, NaN stops; cold: cycle 1 from the terminal guess) ----
+    unsigned long long tp = __builtin_amdgcn_s_memrealtime();
     const double* init_m = secant ? tabm(b_init) : (warm ? tabm(b_cur) : nullptr);
     const double* init_c = secant ? tabc(b_init) : (warm ? tabc(b_cur) : nullptr);
     int final_buf = -1;
@@ -466,17 +521,17 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
         const bool track = n >= 2;
         double dl;
         if (pk == 1)
-          dl = ge_egm_cycle<SMAX, SC, 1>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
-                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+          dl = ge_egm_cycle_fn<SMAX, SC, 1>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                            gam);
         else if (pk == 3)
-          dl = ge_egm_cycle<SMAX, SC, 3>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
-                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+          dl = ge_egm_cycle_fn<SMAX, SC, 3>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                            gam);
         else if (pk == 5)
-          dl = ge_egm_cycle<SMAX, SC, 5>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
-                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+          dl = ge_egm_cycle_fn<SMAX, SC, 5>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                            gam);
         else
-          dl = ge_egm_cycle<SMAX, SC, 0>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta, gam,
-                                         s_Wl, s_Pe, s_hint, lds_v, lds_win);
+          dl = ge_egm_cycle_fn<SMAX, SC, 0>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                            gam);
         // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
         // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
         const bool want_value = ext && n >= kGeExtrap - 1 &&
@@ -566,6 +621,8 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
       __syncthreads();
     }
     if (tid == 0) {
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+      st.t_egm += tn - tp;
       st.cyc_sum += st.n;
       // buffer roles: prev <- cur, cur <- the solve's final tables, the freed ones ping-pong
       const int fb = final_buf;
@@ -578,35 +635,8 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     }
     __syncthreads();
     // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
-    {
-      const double* fm = tabm(st.buf[2]);
-      const double* fc = tabc(st.buf[2]);
-      const bool have_prev = st.steps > 0;
-      ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, fm, fc, R, s_Wl, s_hint, lds_win,
-                         [&](int, int jr, int, int s, double q, double c) {
-                           if (jr >= j1) return;
-                           const double ap = q - c;
-                           const size_t o = (size_t)s * n_a + jr;
-                           int d = -1;
-                           if (have_prev) {   // last evaluation's bracket as the first guess
-                             const int h = LO[o];
-                             if (h >= 0 && h < n_a - 1 && a_grid[h] <= ap && ap < a_grid[h + 1]) d = h;
-                           }
-                           if (d < 0) {       // searchsorted(a_grid, a', 'right') - 1
-                             int lo = 0, hi = n_a;
-                             while (lo < hi) {
-                               const int mid = lo + ((hi - lo) >> 1);
-                               if (a_grid[mid] <= ap) lo = mid + 1; else hi = mid;
-                             }
-                             d = lo - 1;
-                           }
-                           d = d < 0 ? 0 : (d > n_a - 2 ? n_a - 2 : d);
-                           double wl = (a_grid[d + 1] - ap) / (a_grid[d + 1] - a_grid[d]);
-                           wl = wl < 0.0 ? 0.0 : (wl > 1.0 ? 1.0 : wl);
-                           LO[o] = d;
-                           WL[o] = wl;
-                         });
-    }
+    tp = __builtin_amdgcn_s_memrealtime();
+    ge_lottery_fn<SMAX>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
     // ---- the distribution's start (own columns) ----
     if (st.fresh_mass) {
       const double u0 = 1.0 / ((double)S * n_a);
@@ -622,20 +652,31 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
         }
     }
     __syncthreads();
+    if (tid == 0) {
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+      st.t_lot += tn - tp;
+      tp = tn;
+    }
     // ---- the stationary distribution: BiCGSTAB on (I - T) mass = 0 ----
     int mv;
     {
       HkArgs hk;
       hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
-      hk.LO = LO; hk.WL = WL; hk.X = X; hk.Pg = g.pg + row0; hk.Vg = nullptr;
-      hk.slab_cl = g.slab + (size_t)cal * G * 2 * g.cap;
-      hk.span_cl = g.span + (size_t)cal * G * SMAX * 4;
-      hk.ctr = ctr; hk.gran = gran; hk.Pc = g.P + (size_t)cal * S * S;
-      hk.max_iter = g.max_hist; hk.err = g.err;
+      hk.LO = to_global((const int*)LO); hk.WL = to_global((const double*)WL); hk.X = to_global(X);
+      hk.Pg = to_global(g.pg + row0); hk.Vg = to_global((double*)nullptr);
+      hk.slab_cl = to_global(g.slab + (size_t)cal * G * 2 * g.cap);
+      hk.span_cl = to_global(g.span + (size_t)cal * G * SMAX * 4);
+      hk.ctr = to_global(ctr); hk.gran = to_global(gran); hk.Pc = to_global(g.P + (size_t)cal * S * S);
+      hk.max_iter = g.max_hist; hk.err = to_global(g.err);
       hk.tol = st.htol;
-      mv = hk_solve<SMAX, KC, TH>(hk, L, nb, ne);
+      mv = hk_solve_isolated<SMAX, KC, TH>(hk, &nb, &ne);
     }
     if (mv < 0) return;
+    if (tid == 0) {
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+      st.t_hist += tn - tp;
+      tp = tn;
+    }
     // ---- K_s = sum mass a over the cluster ----
     double part = 0.0;
     for (int k = j0 + tid; k < j1; k += TH) {
@@ -658,6 +699,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
       if (!st.refine) st.rs.update(f);
       st.Ks = Ks;
       ++st.steps;
+      st.t_k += __builtin_amdgcn_s_memrealtime() - tp;
     }
     __syncthreads();
   }
@@ -670,6 +712,15 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     g.out_cyc[cal] = (int)min(st.cyc_sum, 0x7fffffffll);
     g.out_its[cal] = (int)min(st.its_sum, 0x7fffffffll);
     g.out_status[cal] = st.status | (st.rs.done ? 0 : 4);
+    double* pf = g.out_prof + (size_t)cal * kGeProf;
+    pf[0] = st.t_egm * 0.01;
+    pf[1] = st.t_lot * 0.01;
+    pf[2] = st.t_hist * 0.01;
+    pf[3] = st.t_k * 0.01;
+    pf[4] = (__builtin_amdgcn_s_memrealtime() - st.t0) * 0.01;
+    pf[5] = (double)st.cyc_sum;
+    pf[6] = (double)st.its_sum;
+    pf[7] = (double)st.steps;
   }
 }
 
@@ -704,9 +755,9 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   if (p.nj > kGeMaxTiles * kTile) return false;
   if ((long long)p.G * n_cal > cus) return false;
   p.kc = p.nj <= th ? 1 : 2;
-  p.smax = 8;
+  p.smax = S == 7 ? 7 : 8;   // the Table II shape: exact state count (fewer registers in the solve)
   p.sc = S == 7 ? 7 : 0;
-  if (p.sc == 7) p.fn = p.kc == 1 ? ge_fn<8, 7, 1>() : ge_fn<8, 7, 2>();
+  if (p.sc == 7) p.fn = p.kc == 1 ? ge_fn<7, 7, 1>() : ge_fn<7, 7, 2>();
   else p.fn = p.kc == 1 ? ge_fn<8, 0, 1>() : ge_fn<8, 0, 2>();
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
@@ -725,7 +776,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, bytes;
+  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, prof, run, bytes;
 };
 static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
   GeScratch L;
@@ -743,6 +794,8 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
   L.cal = take((size_t)n_cal * sizeof(GeCalDev));
   L.outd = take((size_t)n_cal * 3 * sizeof(double));
   L.outi = take((size_t)n_cal * 4 * sizeof(int));
+  L.prof = take((size_t)n_cal * kGeProf * sizeof(double));
+  L.run = take(sizeof(GeRun));
   L.bytes = o;
   return L;
 }
@@ -807,6 +860,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   int* outi = reinterpret_cast<int*>(base + L.outi);
   g.out_r = outd; g.out_K = outd + n_cal; g.out_Ks = outd + 2 * n_cal;
   g.out_steps = outi; g.out_cyc = outi + n_cal; g.out_its = outi + 2 * n_cal; g.out_status = outi + 3 * n_cal;
+  g.out_prof = reinterpret_cast<double*>(base + L.prof);
   AIY_HIP(h, hipMemcpyAsync(base + L.cal, cals.data(), sizeof(GeCalDev) * n_cal, hipMemcpyHostToDevice, st));
   AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n_cal * kHcCtrStride * sizeof(unsigned), st));
   AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n_cal * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
@@ -823,6 +877,9 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   AIY_HIP(h, hipMemcpyAsync(&err, g.err, sizeof(unsigned), hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(hd.data(), outd, sizeof(double) * 3 * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(hi.data(), outi, sizeof(int) * 4 * n_cal, hipMemcpyDeviceToHost, st));
+  h->ge_prof.assign((size_t)n_cal * kGeProf, 0.0);
+  AIY_HIP(h, hipMemcpyAsync(h->ge_prof.data(), g.out_prof, sizeof(double) * kGeProf * n_cal, hipMemcpyDeviceToHost,
+                            st));
   AIY_HIP(h, hipStreamSynchronize(st));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, h->ge_ev[0], h->ge_ev[1]) == hipSuccess) {
@@ -882,4 +939,16 @@ extern "C" int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* l
     h->ge_egm_cycles = 0.0;
   }
   return AIY_OK;
+}
+
+// Per-calibration profile of the last device-resident GE launch (measurement hook):
+// out[c * 8 + k] for k = EGM, lottery, distribution solve, K reduction + search, whole
+// search (microseconds, workgroup 0's clock), EGM cycles, matvecs, evaluations.  Returns
+// the calibrations written (<= n_cal).  Host-only.
+extern "C" int32_t aiy_ge_last_profile(aiy_handle* h, double* out, int32_t n_cal) {
+  if (!h || !out || n_cal < 0) return AIY_ERR_ARG;
+  const int have = (int)(h->ge_prof.size() / kGeProf);
+  const int n = std::min(have, (int)n_cal);
+  std::copy(h->ge_prof.begin(), h->ge_prof.begin() + (size_t)n * kGeProf, out);
+  return n;
 }

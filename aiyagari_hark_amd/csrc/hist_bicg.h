@@ -62,21 +62,23 @@ struct HkShared {
 // One calibration's BiCGSTAB distribution solve by the workgroups of its cluster (this
 // workgroup: w of G, own columns [j0, j1)); shared by hist_bicg_kernel (one solve per
 // launch) and the device-resident GE search (ge_resident.hip, many solves per launch).
+// (pointers typed global: hk_solve_isolated receives them as plain arguments, where the
+// compiler could not infer their address space and would use flat accesses)
 struct HkArgs {
   int G, S, n_a, cap, w, j0, j1;
-  const int* LO;          // [S][n_a] lottery of the calibration (index)
-  const double* WL;       // [S][n_a] lottery weight on lo
-  double* X;              // [S][n_a] in: start, out: T x (own columns)
-  double* Pg;             // [S][n_a] p scratch rows
-  double* Vg;             // v block of this workgroup in HBM (SMAX > 8)
-  double* slab_cl;        // [G][2][cap]
-  int* span_cl;           // [G][SMAX][4]
-  unsigned* ctr;          // cluster barrier counter
-  unsigned long long* gran;   // [2][G][kHcRedRec] reduction granules
-  const double* Pc;       // [S][S]
+  gptr<const int> LO;          // [S][n_a] lottery of the calibration (index)
+  gptr<const double> WL;       // [S][n_a] lottery weight on lo
+  gptr<double> X;              // [S][n_a] in: start, out: T x (own columns)
+  gptr<double> Pg;             // [S][n_a] p scratch rows
+  gptr<double> Vg;             // v block of this workgroup in HBM (SMAX > 8)
+  gptr<double> slab_cl;        // [G][2][cap]
+  gptr<int> span_cl;           // [G][SMAX][4]
+  gptr<unsigned> ctr;          // cluster barrier counter
+  gptr<unsigned long long> gran;   // [2][G][kHcRedRec] reduction granules
+  gptr<const double> Pc;       // [S][S]
   double tol;
   int max_iter;
-  unsigned* err;
+  gptr<unsigned> err;
 };
 
 // Returns the matvecs of the solve, or -1 when the cluster stops (error word set: a
@@ -108,14 +110,15 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   const int w = r.w;
   const int j0 = r.j0;
   const int j1 = r.j1;
-  unsigned* ctr = r.ctr;
-  unsigned long long* gran = r.gran;
-  const int* LO = r.LO;
-  const double* WL = r.WL;
-  double* X = r.X;   // x: the iterate, own columns read-modify-written
-  double* slab_cl = r.slab_cl;
-  const double* __restrict__ Pc = r.Pc;
-  int* span_cl = r.span_cl;
+  unsigned* ctr = (unsigned*)r.ctr;
+  unsigned long long* gran = (unsigned long long*)r.gran;
+  const int* LO = (const int*)r.LO;
+  const double* WL = (const double*)r.WL;
+  double* X = (double*)r.X;   // x: the iterate, own columns read-modify-written
+  double* slab_cl = (double*)r.slab_cl;
+  const double* __restrict__ Pc = (const double*)r.Pc;
+  int* span_cl = (int*)r.span_cl;
+  unsigned* err = (unsigned*)r.err;
 
   // ---- setup (as hist_cluster_kernel): P, own spans, covering candidates ----
   for (int q = tid; q < SMAX * SMAX; q += TH) {
@@ -136,22 +139,22 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       s_pub[2 * s + 1][0] = tot + min(ll, max(0, j1 - f));
       s_pub[2 * s + 1][1] = tot + ll;
       int* sp = &span_cl[((size_t)w * SMAX + s) * 4];
-      __hip_atomic_store(&sp[0], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sp[1], ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sp[2], tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[0]), f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[1]), ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[2]), tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       tot += ll;
     }
     s_tot = tot;
     if (tot > cap) bad = 2u;
-    if (bad) __hip_atomic_store(r.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   auto barrier = [&]() -> bool {
     ++nb;
-    return hc_barrier(r.err, ctr, (unsigned)G * nb, &s_flag);
+    return hc_barrier(err, ctr, (unsigned)G * nb, &s_flag);
   };
   if (!barrier()) return -1;
-  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
   if (s_stop) return -1;
   if (tid < S) {
@@ -159,10 +162,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     int n = 0, bad = 0;
     for (int w2 = 0; w2 < G; ++w2) {
       const int* sp = &span_cl[((size_t)w2 * SMAX + s) * 4];
-      const int f = __hip_atomic_load(&sp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int l = __hip_atomic_load(&sp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int f = __hip_atomic_load(to_global(&sp[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int l = __hip_atomic_load(to_global(&sp[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (f < j1 && f + l > j0) {
-        const int base = __hip_atomic_load(&sp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int base = __hip_atomic_load(to_global(&sp[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, base};
         else bad = 1;
         ++n;
@@ -170,14 +173,14 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     }
     s_ncand[s] = n < kHcCand ? n : kHcCand;
     if (bad) {
-      __hip_atomic_store(r.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(err), 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   const int total = s_tot;
   for (int q = tid; q < total; q += TH) Tacc[q] = 0.0;
   if (!barrier()) return -1;
-  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
   if (s_stop) return -1;
 #pragma unroll
@@ -434,8 +437,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, s_part[v][q]) : x + s_part[v][q];
       const unsigned long long b = (unsigned long long)__double_as_longlong(x);
       unsigned long long* g = slot + (size_t)w * (2 * kHkRed) + 2 * v;
-      __hip_atomic_store(g, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 1, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     prefetch();   // loads the step after the reduction needs, in flight across the sweep
     if (wid == 0) {
@@ -452,8 +455,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             double x = 0.0;
             if (v < nv && w2 < G) {
               const unsigned long long* g = slot + (size_t)w2 * (2 * kHkRed) + 2 * v;
-              const unsigned long long hi = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              const unsigned long long lo = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long hi = __hip_atomic_load(to_global(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long lo = __hip_atomic_load(to_global(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
               x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
             }
@@ -464,7 +467,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-          if (lane == 0) __hip_atomic_store(r.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(to_global(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       } while (true);
@@ -489,8 +492,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   double rv[KC][SMAX], pv[KC][SMAX], tv[KC][SMAX];
   // v: in LDS behind the spans when it fits (SMAX <= 8), else a per-workgroup HBM block of
   // the same [KC][SMAX][TH] layout (behind the p rows of the scratch)
-  double* Vl = kVlds ? Tacc + cap : r.Vg;
-  double* Pg = r.Pg;
+  double* Vl = kVlds ? Tacc + cap : (double*)r.Vg;
+  double* Pg = (double*)r.Pg;
   auto vidx = [&](int k, int s) { return (k * SMAX + s) * TH + tid; };
   double part[kHkRed];
   const double tol = r.tol;
@@ -689,6 +692,32 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
            (int)blockIdx.x, G, j1 - j0, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv, ph[3] * 0.01 / mv,
            ph[4] * 0.01 / mv, ph[5] * 0.01 / mv);
 #endif
+  return mv;
+}
+
+// hk_solve as its own (not inlined) function with its LDS declared here: a caller that
+// carries a lot of live state of its own (ge_resident.hip's search loop) would otherwise
+// force the solve's registers into scratch; the call costs a few register saves per
+// solve.  The span buffer / v share the caller's dynamic LDS.
+template <int SMAX, int KC, int TH>
+__device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
+  extern __shared__ double hk_dyn[];
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  const HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop};
+  unsigned nb = *nb_io, ne = *ne_io;
+  const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
+  *nb_io = nb;
+  *ne_io = ne;
   return mv;
 }
 

@@ -48,13 +48,13 @@ struct HcCand {
 __device__ __forceinline__ bool hc_barrier(unsigned* err, unsigned* ctr, unsigned target, int* s_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(to_global(ctr), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int ok = 1;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(to_global(ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(to_global(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
       }
@@ -78,16 +78,16 @@ __device__ __forceinline__ bool hc_barrier_count(unsigned* err, unsigned long lo
                                                  unsigned flag, unsigned* nc_out, int* s_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long v = __hip_atomic_fetch_add(cw, 1ull | ((unsigned long long)flag << 32), __ATOMIC_RELAXED,
+    unsigned long long v = __hip_atomic_fetch_add(to_global(cw), 1ull | ((unsigned long long)flag << 32), __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT) +
                            (1ull | ((unsigned long long)flag << 32));
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int ok = 1;
     while ((unsigned)v < target) {
       __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = __hip_atomic_load(to_global(cw), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(to_global(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
       }

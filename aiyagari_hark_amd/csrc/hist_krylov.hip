@@ -63,19 +63,19 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   a.G = G; a.S = S; a.n_a = n_a; a.cap = r.cap; a.w = w;
   a.j0 = w * r.nj;
   a.j1 = min(a.j0 + r.nj, n_a);
-  a.LO = r.lo + row0 * n_a;
-  a.WL = r.wlo + row0 * n_a;
-  a.X = r.mass + row0 * n_a;
-  a.Pg = r.dbuf + row0 * n_a;
-  a.Vg = SMAX <= 8 ? nullptr : r.dbuf + (size_t)r.n_cal * S * n_a + (size_t)blockIdx.x * (KC * SMAX * TH);
-  a.slab_cl = r.slab + (size_t)lc * G * 2 * r.cap;
-  a.span_cl = r.span + (size_t)lc * G * SMAX * 4;
-  a.ctr = r.ctr + (size_t)lc * kHcCtrStride;
-  a.gran = reinterpret_cast<unsigned long long*>(r.dist) + (size_t)lc * 2 * G * kHcRedRec;
-  a.Pc = r.P + (size_t)cal * S * S;
+  a.LO = to_global(r.lo + row0 * n_a);
+  a.WL = to_global(r.wlo + row0 * n_a);
+  a.X = to_global(r.mass + row0 * n_a);
+  a.Pg = to_global(r.dbuf + row0 * n_a);
+  a.Vg = to_global(SMAX <= 8 ? nullptr : r.dbuf + (size_t)r.n_cal * S * n_a + (size_t)blockIdx.x * (KC * SMAX * TH));
+  a.slab_cl = to_global(r.slab + (size_t)lc * G * 2 * r.cap);
+  a.span_cl = to_global(r.span + (size_t)lc * G * SMAX * 4);
+  a.ctr = to_global(r.ctr + (size_t)lc * kHcCtrStride);
+  a.gran = to_global(reinterpret_cast<unsigned long long*>(r.dist) + (size_t)lc * 2 * G * kHcRedRec);
+  a.Pc = to_global(r.P + (size_t)cal * S * S);
   a.tol = r.tolv ? r.tolv[cal] : r.tol;
   a.max_iter = r.max_iter;
-  a.err = r.err;
+  a.err = to_global(r.err);
   unsigned nb = 0, ne = 0;
   const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;

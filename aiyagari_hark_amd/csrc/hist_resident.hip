@@ -115,14 +115,14 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
       s_pub[2 * s + 1][0] = tot + min(ll, max(0, j1 - f));
       s_pub[2 * s + 1][1] = tot + ll;
       int* sp = &span_cl[((size_t)w * SMAX + s) * 4];
-      __hip_atomic_store(&sp[0], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sp[1], ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sp[2], tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[0]), f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[1]), ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&sp[2]), tot - f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       tot += ll;
     }
     s_tot = tot;
     if (tot > cap) bad = 2u;
-    if (bad) __hip_atomic_store(r.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bad) __hip_atomic_store(to_global(r.err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   double m[KC][SMAX];
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     for (int s = 0; s < SMAX; ++s) m[k][s] = (s < S && j < j1) ? MS[(size_t)s * n_a + j] : 0.0;
   }
   if (!hc_barrier(r, ctr, (unsigned)G, &s_flag)) return;
-  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (tid == 0) s_stop = __hip_atomic_load(to_global(r.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
   if (s_stop) return;
   // covering workgroups of every row for this workgroup's columns, ascending w
@@ -142,10 +142,10 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     int n = 0, bad = 0;
     for (int w2 = 0; w2 < G; ++w2) {
       const int* sp = &span_cl[((size_t)w2 * SMAX + s) * 4];
-      const int f = __hip_atomic_load(&sp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int l = __hip_atomic_load(&sp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int f = __hip_atomic_load(to_global(&sp[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int l = __hip_atomic_load(to_global(&sp[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (f < j1 && f + l > j0) {
-        const int base = __hip_atomic_load(&sp[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int base = __hip_atomic_load(to_global(&sp[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n < kHcCand) s_cand[s][n] = HcCand{w2, f, l, base};
         else bad = 1;
         ++n;
@@ -153,14 +153,14 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
     }
     s_ncand[s] = n < kHcCand ? n : kHcCand;
     if (bad) {
-      __hip_atomic_store(r.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(r.err), 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   const int total = s_tot;
   for (int q = tid; q < total; q += TH) Tacc[q] = 0.0;
   if (!hc_barrier(r, ctr, 2u * G, &s_flag)) return;
-  if (tid == 0) s_stop = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (tid == 0) s_stop = __hip_atomic_load(to_global(r.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
   if (s_stop) return;
   // per (column, row): first covering candidate and how many cover it (fixed for the

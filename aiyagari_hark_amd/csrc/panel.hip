@@ -181,11 +181,11 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
     const int ng = nb < kTicketGroups ? nb : kTicketGroups;
     const int g = blockIdx.x % kTicketGroups;
     const int gsize = (nb - g + kTicketGroups - 1) / kTicketGroups;
-    const unsigned prev = __hip_atomic_fetch_add(&r.ticket[g * kTicketStride], 1u, __ATOMIC_RELAXED,
+    const unsigned prev = __hip_atomic_fetch_add(to_global(&r.ticket[g * kTicketStride]), 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     is_last = 0;
     if (prev == (unsigned)gsize - 1) {
-      const unsigned top = __hip_atomic_fetch_add(&r.ticket[kTicketGroups * kTicketStride], 1u, __ATOMIC_RELAXED,
+      const unsigned top = __hip_atomic_fetch_add(to_global(&r.ticket[kTicketGroups * kTicketStride]), 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
       is_last = (top == (unsigned)ng - 1) ? 1 : 0;
     }
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kSimBlock) void sim_period_kernel(PanelDev P, Panel
   if (threadIdx.x == 0) {
     const double total = (red[0] + red[1]) + (red[2] + red[3]);
     for (int g = 0; g <= kTicketGroups; ++g)
-      __hip_atomic_store(&r.ticket[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(&r.ticket[g * kTicketStride]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (r.finish) mill(mk, P.mrkv_hist, r.n_total, total, r.sow, r.hist_A, r.hist_M);
     else store_f64_agent(&r.sow[6], total);
   }

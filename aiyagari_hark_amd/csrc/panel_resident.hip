@@ -238,9 +238,9 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
       double sb = 0.0;
       for (int w = 0; w < nthr / kWave; ++w) sb += s_red[w];
       const unsigned long long bits = (unsigned long long)__double_as_longlong(sb);
-      __hip_atomic_store(&gslot[2 * blockIdx.x], ((unsigned long long)e << 32) | (bits >> 32), __ATOMIC_RELAXED,
+      __hip_atomic_store(to_global(&gslot[2 * blockIdx.x]), ((unsigned long long)e << 32) | (bits >> 32), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gslot[2 * blockIdx.x + 1], ((unsigned long long)e << 32) | (bits & 0xffffffffull),
+      __hip_atomic_store(to_global(&gslot[2 * blockIdx.x + 1]), ((unsigned long long)e << 32) | (bits & 0xffffffffull),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- 3. next period's labour draws overlap the exchange (waves 1..; wave 0 sweeps) ----
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
         for (int k = 0; k < kResGranPerLane; ++k) {
           const int gi = tid * kResGranPerLane + k;
           if (gi < 2 * nb) {
-            gv[k] = __hip_atomic_load(&gslot[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gv[k] = __hip_atomic_load(to_global(&gslot[gi]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             all = all && (unsigned)(gv[k] >> 32) == e;
           } else {
             gv[k] = 0;
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
       if (tid == 0) {
-        if (!ok) __hip_atomic_store(r.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok) __hip_atomic_store(to_global(r.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_abort = ok ? 0 : 1;
         last = calc_prices(mk, mrkv_next, acc / (double)r.n);   // np.mean(np.array(aNow))
         s_price[0] = last.Mnow;

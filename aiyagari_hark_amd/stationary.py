@@ -255,12 +255,34 @@ class _Brent:
         self.x = xcur
 
 
+def resident_plan(device, n_cal, S, n_a, cu_share=1.0):
+    """(G, columns per workgroup, columns per thread, blocks) of the device-resident GE
+    search (aiy_ge_resident_plan, csrc/ge_resident.hip) for this shape, or None when
+    aiy_ge_stationary would run the host-driven loop instead."""
+    dev = _resolve_device(device)
+    h = _lib.handle(dev.index)
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 1), "aiy_set_option")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, _cu_limit(dev, cu_share)), "aiy_set_option")
+    out = (ctypes.c_int32 * 4)()
+    ok = h.lib.aiy_ge_resident_plan(h.h, int(n_cal), int(S), int(n_a), out)
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 0), "aiy_set_option")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, 0), "aiy_set_option")
+    return tuple(out) if ok == 1 else None
+
+
+def _cu_limit(dev, cu_share):
+    return 0 if float(cu_share) >= 1.0 else _device_cus(dev, cu_share)
+
+
 def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hist, warm_egm, accel, r_lo=None,
-                         r_hi=None, secant=False, loose=False, extrapolate=False, handle=None, stream=None):
+                         r_hi=None, secant=False, loose=False, extrapolate=False, handle=None, stream=None,
+                         resident=False, cu_share=1.0):
     """The whole E1 search in ONE library call (aiy_ge_stationary: the bracket updates run
-    in C++ between device K_s evaluations).  Returns (r, K, Ks, steps, egm_cycles_sum,
-    hist_iters_sum).  handle / stream: a library handle and torch stream of the caller's
-    (default: the device's shared handle, the current stream)."""
+    in C++ between device K_s evaluations, or -- resident=True, where the shape allows --
+    the whole search of every calibration in one device-resident launch).  Returns (r, K,
+    Ks, steps, egm_cycles_sum, hist_iters_sum, status).  handle / stream: a library handle
+    and torch stream of the caller's (default: the device's shared handle, the current
+    stream)."""
     n = len(b.cals)
     h = handle if handle is not None else _lib.handle(b.device.index)
     work = torch.empty(int(h.lib.aiy_ge_stationary_work_bytes(n, b.S, b.n_a)), dtype=torch.uint8, device=b.device)
@@ -281,10 +303,16 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
     opt.status_out = ctypes.addressof(status)
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-    h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
-                                    ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its),
-                                    _lib.stream_ptr(stream)),
-            "aiy_ge_stationary")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, int(bool(resident))), "aiy_set_option")
+    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, _cu_limit(b.device, cu_share)), "aiy_set_option")
+    try:
+        h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
+                                        ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its),
+                                        _lib.stream_ptr(stream)),
+                "aiy_ge_stationary")
+    finally:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 0), "aiy_set_option")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, 0), "aiy_set_option")
     return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value),
             np.array(status[:], dtype=np.int32))
 
@@ -365,7 +393,7 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
 def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=1e-7, egm_tol=1e-8,
                  hist_tol=1e-12, device=None, r_lo=None, r_hi=None, max_steps=60, log=None, warm_hist=True,
                  method="bisect", warm_egm=None, accel=None, engine="native", secant=None, loose=None,
-                 extrapolate=None, groups=None, cu_share=1.0):
+                 extrapolate=None, groups=None, cu_share=1.0, resident=None):
     """GE on r (E1) for every calibration at once.  Returns StationaryResult.
 
     method: "bisect" -- bisection on K_s(r) - K_d(r) to bracket width r_tol (the oracle's
@@ -397,7 +425,12 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     streams and host threads (_solve_groups; 3 groups fill the process's hardware queues
     beside the default stream -- 4 measured slower).  cu_share: the fraction of the
     device's compute units this process's resident clusters may hold (several rank
-    processes on one GPU: 1 / ranks), so that every process's clusters stay co-resident."""
+    processes on one GPU: 1 / ranks), so that every process's clusters stay co-resident.
+    resident (native only; default: wherever resident_plan() has a plan, with the BiCGSTAB
+    distribution solve): the whole search of every calibration in ONE device-resident
+    launch (csrc/ge_resident.hip: each calibration's cluster runs its own EGM cycles,
+    lottery, BiCGSTAB and root search, no host round trip, no waiting for other
+    calibrations); groups are then 1."""
     cals = table2_calibrations() if cals is None else list(cals)
     device = _resolve_device(device)
     aGrid = sm.make_grid_exp_mult(aMin, aMax, n_a, aNestFac)
@@ -411,6 +444,12 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
         loose = method == "brent"
     if extrapolate is None:
         extrapolate = method == "brent"
+    if resident is None:
+        resident = (engine == "native" and log is None and accel < 0 and
+                    resident_plan(device, len(cals), cals[0].LaborStatesNo, n_a, cu_share) is not None)
+    resident = bool(resident) and engine == "native" and log is None
+    if resident:
+        groups = 1
     if groups is None:
         groups = 3 if (method == "brent" and engine == "native" and log is None and len(cals) >= 3) else 1
     if groups > 1:
@@ -438,7 +477,8 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
                                                                 warm_hist, warm_egm, accel, r_lo if r_lo is not None
                                                                 else None, r_hi if r_hi is not None else None,
                                                                 secant=secant and warm_hist and warm_egm,
-                                                                loose=loose, extrapolate=extrapolate)
+                                                                loose=loose, extrapolate=extrapolate,
+                                                                resident=resident, cu_share=cu_share)
         KtoY = K ** (1.0 - b.alpha)
         return StationaryResult(r=r, K=K, K_supply=Ks, KtoY=KtoY, saving_rate=b.delta * KtoY, bisection_steps=steps,
                                 egm_cycles=[np.array([cyc_sum])], hist_iters=[np.array([it_sum])], status=status)

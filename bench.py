@@ -50,6 +50,7 @@ HIST_BYTES_PER_POINT = 28      # mass in 8, lottery index 4, wei
 # the 28 B of the push/mix matvec plus half an iteration's iterate traffic (x read and
 # written twice, p written and read: 48 B per iteration of two matvecs)
 HIST_BYTES_PER_POINT_KRYLOV = 52
+EGM_BYTES_PER_NODE_CYCLE = 32  # SURVEY.md §8d stationary EGM: read (m, c) next + write (m, c) new per node
 N_AGENTS = 1_000_006           # nearest multiple of 7 >= 1e6
 N_AGENTS_C3 = 99_999_998       # 1e8 agents, multiple of 7
 T_C3 = 1000
@@ -144,6 +145,20 @@ def gather_objects(obj, world):
     return out
 
 
+def ge_stats(h, reset, dev=None):
+    """Device-resident GE launches (csrc/ge_resident.hip) since the last reset, summed over
+    the device's handles: (kernel ms by HIP events, launches, point-matvecs, EGM cycles)."""
+    from aiyagari_hark_amd import stationary
+    hs = [h] + [hg for (d, _), (hg, _) in stationary._GROUP_CTX.items() if dev is None or d == dev.index]
+    tot = [0.0, 0, 0.0, 0.0]
+    for hh in hs:
+        ms, n, pts, cyc = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        hh.check(hh.lib.aiy_ge_launch_stats(hh.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(pts),
+                                            ctypes.byref(cyc), int(reset)), "ge stats")
+        tot = [tot[0] + ms.value, tot[1] + n.value, tot[2] + pts.value, tot[3] + cyc.value]
+    return tuple(tot)
+
+
 def hist_stats(h, reset, dev=None):
     """Resident-histogram kernel milliseconds and launches since the last reset, summed
     over the device's shared handle and the handles of solve_table2's independent groups
@@ -179,6 +194,7 @@ def table2_leg(args, world, rank, dev):
     for _ in range(args.warmup):
         sweep()
     hist_stats(h, True, dev)
+    ge_stats(h, True, dev)
     point_iters = 0   # (state, node) points x matvecs of the distribution solves
     res = None
     barrier(world)
@@ -189,9 +205,19 @@ def table2_leg(args, world, rank, dev):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     hist_ms, hist_n = hist_stats(h, True, dev)
-    # dominant kernel: the device-resident BiCGSTAB distribution solve (one launch per K_s(r)
-    # evaluation); algorithmic bytes 52 per (state, node) point per matvec
-    hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
+    ge_ms, ge_n, ge_pts, ge_cyc = ge_stats(h, True, dev)
+    if ge_n > 0:
+        # dominant kernel: the device-resident GE search (one launch per sweep): algorithmic
+        # bytes = 52 per (state, node) point per matvec of the distribution solves + 32 S
+        # (N_a + 1) per calibration and EGM cycle
+        kern = "ge_cluster_kernel (device-resident GE search: EGM cycles + lottery + BiCGSTAB + root search)"
+        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * ge_pts + EGM_BYTES_PER_NODE_CYCLE * 7 * (args.grid + 1) * ge_cyc
+        hist_ms, hist_n = ge_ms, ge_n
+    else:
+        # dominant kernel: the device-resident BiCGSTAB distribution solve (one launch per
+        # K_s(r) evaluation); algorithmic bytes 52 per (state, node) point per matvec
+        kern = "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery stationary distribution)"
+        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
     hist_gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[float(x) for x in res.r], KtoY=[float(x) for x in res.KtoY],
                                    evaluations=res.bisection_steps), world)
@@ -200,7 +226,8 @@ def table2_leg(args, world, rank, dev):
     for pr in per_rank:
         for k, rr, ky in zip(pr["cells"], pr["r"], pr["KtoY"]):
             r[k], kty[k] = rr, ky
-    out = dict(seconds_per_sweep=el / args.steps, value=len(cells) * args.steps / el,
+    out = dict(seconds_per_sweep=el / args.steps, value=len(cells) * args.steps / el, kernel=kern,
+               resident=ge_n > 0, egm_cycles_per_sweep=ge_cyc / args.steps if ge_n else None,
                hist_kernel_ms_per_sweep=hist_ms / args.steps, hist_launches_per_sweep=hist_n / args.steps,
                hist_gbs=hist_gbs, hist_bytes_per_launch=hist_bytes / max(1, hist_n),
                hist_avg_launch_ms=hist_ms / max(1, hist_n),
@@ -686,18 +713,23 @@ def main():
                                "Young-lottery stationary distribution; one step = the whole sweep",
                    "calibrations": N_TABLE2, "n_a": args.grid, "S": 7,
                    "parallelism": f"calibrations split round-robin over {world} rank(s), no data-path collective; "
-                                  "per GPU 3 independent root searches (own handle, stream, host thread)"},
-        "roofline": {"kernel": "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery "
-                               "stationary distribution)", "bound": "hbm",
+                                  + ("per GPU one device-resident launch, a cluster of workgroups per calibration "
+                                     "running its whole root search" if t2["resident"] else
+                                     "per GPU 3 independent root searches (own handle, stream, host thread)")},
+        "roofline": {"kernel": t2["kernel"], "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
                      "traffic": pmc_traffic("hist_bicg_kernel",
                                             scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV),
                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
                      "avg_launch_ms": t2["hist_avg_launch_ms"],
-                     "launch": "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
-                               "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
-                               "updates)",
+                     "launch": ("one whole sweep of the rank's calibrations (every K_s(r) evaluation of every "
+                                "root search): 52 B per state x node point per matvec of the distribution solves "
+                                "(28 B lottery push + mix, 24 B iterate updates) + 32 B per state x node per EGM "
+                                "cycle" if t2["resident"] else
+                                "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
+                                "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
+                                "updates)"),
                      "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"]),
                      # concurrent launches (independent groups) overlap: the device-level rate is the
                      # algorithmic bytes of a whole sweep over the sweep's wall time
@@ -705,7 +737,8 @@ def main():
                                           "frac": sweep_bytes / t2["seconds_per_sweep"] / 1e9 / HBM_PEAK_GBS,
                                           "note": "algorithmic bytes of all launches of a sweep / sweep wall time"}},
         "table2": {k: t2[k] for k in ("seconds_per_sweep", "evaluations_rank0", "hist_launches_per_sweep",
-                                      "hist_kernel_ms_per_sweep", "r_percent", "saving_rate_percent")},
+                                      "hist_kernel_ms_per_sweep", "resident", "egm_cycles_per_sweep", "r_percent",
+                                      "saving_rate_percent")},
         "cpu_baseline": None,
     }
     if args.dist_backend == "gloo" and world > 1:

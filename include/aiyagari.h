@@ -451,6 +451,12 @@ int32_t aiy_ge_resident_plan(aiy_handle* h, int32_t n_cal, int32_t S, int32_t n_
 int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, double* point_matvecs,
                             double* egm_cycles, int32_t reset);
 
+/* Per-calibration profile of the last device-resident GE launch (measurement hook):
+ * out[c * 8 + k], k = EGM, lottery, distribution solve, K reduction + search, whole search
+ * (microseconds, workgroup 0's clock), EGM cycles, matvecs, evaluations.  Returns the
+ * calibrations written (<= n_cal).  Host-only. */
+int32_t aiy_ge_last_profile(aiy_handle* h, double* out, int32_t n_cal);
+
 /* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
  * the device-resident distribution-iteration launches since the last reset (HIP events on
  * their stream) and their number.  reset != 0 zeroes the counters.  Host-only. */

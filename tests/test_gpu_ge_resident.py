@@ -1,0 +1,74 @@
+"""GPU tests of the device-resident GE search (csrc/ge_resident.hip):
+every calibration's cluster runs its whole root search -- EGM cycles, lottery, BiCGSTAB
+distribution solve, K_s reduction, Brent / bisection update -- inside ONE launch.
+
+* the same search as the host-driven loop (aiy_ge_stationary with AIY_OPT_GE_RESIDENT off):
+  bisection takes the same steps and lands on the same r; Brent lands within the search
+  tolerance of it (the two paths sum K_s in different orders, so a near-tie can take a
+  different Brent step);
+* the oracle's full-size Table II roots are pinned in test_gpu_benchsize.py (the bench's
+  call, which takes this path by default).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cells(n):
+    from aiyagari_hark_amd.stationary import table2_calibrations
+    cals = table2_calibrations()
+    return [cals[k] for k in np.linspace(0, len(cals) - 1, n).astype(int)]
+
+
+def test_resident_plan_shapes(gpu):
+    from aiyagari_hark_amd.stationary import resident_plan
+    p = resident_plan(gpu, 24, 7, 10_000)
+    assert p is not None
+    G, nj, kc, blocks = p
+    assert G * 24 <= torch.cuda.get_device_properties(gpu).multi_processor_count
+    assert G * nj >= 10_000 and kc in (1, 2) and blocks % 8 == 0
+    p3 = resident_plan(gpu, 3, 7, 10_000)
+    assert p3 is not None and p3[0] >= G
+    half = resident_plan(gpu, 24, 7, 10_000, cu_share=0.5)
+    assert half is None or half[0] * 24 <= 128
+    assert resident_plan(gpu, 3, 25, 50_000) is None     # stress shape: the host loop
+
+
+@pytest.mark.parametrize("method", ["bisect", "brent"])
+def test_resident_matches_host_search(gpu, method):
+    from aiyagari_hark_amd.stationary import solve_table2
+    cals = _cells(6)
+    kw = dict(n_a=1500, device=gpu, method=method, accel=-1, warm_egm=True, groups=1)
+    res = solve_table2(cals, resident=True, **kw)
+    ref = solve_table2(cals, resident=False, **kw)
+    print(f"\n{method}: resident r {res.r} steps {res.bisection_steps}; host r {ref.r} steps {ref.bisection_steps}")
+    assert np.all(res.status == 0) and np.all(ref.status == 0)
+    if method == "bisect":
+        assert res.bisection_steps == ref.bisection_steps
+        assert np.max(np.abs(res.r - ref.r)) <= 1e-12
+    else:
+        assert np.max(np.abs(res.r - ref.r)) <= 2e-7
+    assert np.max(np.abs(res.KtoY - ref.KtoY) / ref.KtoY) <= 2e-6
+
+
+def test_resident_default_sweep_and_stats(gpu):
+    """solve_table2(method="brent") takes the resident path by default; its launch is
+    counted by aiy_ge_launch_stats (the bench's roofline source)."""
+    import ctypes
+
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    h = _lib.handle(gpu.index)
+    h.check(h.lib.aiy_ge_launch_stats(h.h, None, None, None, None, 1), "reset")
+    res = solve_table2(table2_calibrations(), n_a=2000, device=gpu, method="brent")
+    ms, n, pts, cyc = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+    h.check(h.lib.aiy_ge_launch_stats(h.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(pts), ctypes.byref(cyc), 1),
+            "stats")
+    print(f"\nresident sweep at N_a = 2000: {ms.value:.2f} ms in {n.value} launch(es), {pts.value:.3e} point-matvecs, "
+          f"{cyc.value:.0f} EGM cycles; r = {np.round(100 * res.r, 5)}")
+    assert n.value == 1 and ms.value > 0 and pts.value > 0 and cyc.value > 0
+    assert np.all(res.status == 0)
+    ref = solve_table2(table2_calibrations(), n_a=2000, device=gpu, method="brent", resident=False)
+    assert np.max(np.abs(res.r - ref.r)) <= 2e-7
