@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU call that runs a list of steps in order, each under its own time limit, and stops
+# at the first step that fails, times out or crashes (no GPU work after a fault).
+#   bash tools/gpu_session.sh TAG step [step ...]
+# steps: resident | profile | nlab | suite | bench | benchsize
+set -u
+TAG=$1
+shift
+mkdir -p gpurun_out
+run() {   # name seconds command...
+  local name=$1 secs=$2
+  shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/${TAG}_${name}.out" 2> "gpurun_out/${TAG}_${name}.err"
+  local rc=$?
+  echo "[session] $name rc=$rc"
+  tail -3 "gpurun_out/${TAG}_${name}.out"
+  if [ $rc -ne 0 ]; then
+    tail -20 "gpurun_out/${TAG}_${name}.err"
+    exit $rc
+  fi
+}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  case $step in
+    resident) run resident 300 $PYT tests/test_gpu_ge_resident.py ;;
+    profile) run profile 300 python -u tools/ge_resident_profile.py ;;
+    nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
+    benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
+    suite) run suite 1000 $PYT -m gpu tests ;;
+    bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
+    bench_t2) run bench_t2 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[session] done"
