@@ -621,19 +621,22 @@ def test_stationary_brent_warm_matches_oracle_bisection(gpu):
 @pytest.mark.parametrize("method", ["bisect", "brent"])
 def test_native_ge_search_equals_python_loop(gpu, method):
     """aiy_ge_stationary (the E1 search loop in C++) takes exactly the steps of
-    the Python-driven loop: identical r (bit for bit) and step count."""
+    the Python-driven loop: identical r (bit for bit) and step count.  The host-driven native
+    loop is the one compared bit for bit; the device-resident search (one launch, its own
+    cluster sizes and so its own reduction order) reaches the same root to the tolerance."""
     from aiyagari_hark_amd.stationary import Calibration, solve_table2
     cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0),
             Calibration(LaborAR=0.3, LaborSD=0.4, CRRA=3.0)]
     nat = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="native", secant=False,
-                       loose=False, extrapolate=False, groups=1)
+                       loose=False, extrapolate=False, groups=1, resident=False)
     py = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="python")
     assert nat.bisection_steps == py.bisection_steps
     assert np.array_equal(nat.r, py.r)
     assert np.array_equal(nat.KtoY, py.KtoY)
     if method == "brent":   # secant starts: other iterates, the same root to the search tolerance
-        for sec_on, loose_on, ex_on, grp in ((True, False, False, 1), (True, True, False, 1), (True, True, True, 1),
-                                             (True, True, True, 3)):
+        for sec_on, loose_on, ex_on, grp, res in ((True, False, False, 1, False), (True, True, False, 1, False),
+                                                  (True, True, True, 1, False), (True, True, True, 3, False),
+                                                  (False, False, False, 1, True), (True, True, True, 1, True)):
             sec = solve_table2(cals, n_a=300, r_tol=1e-8, device=gpu, method=method, engine="native",
-                               secant=sec_on, loose=loose_on, extrapolate=ex_on, groups=grp)
+                               secant=sec_on, loose=loose_on, extrapolate=ex_on, groups=grp, resident=res)
             assert np.max(np.abs(sec.r - py.r)) < 1e-7, (sec_on, loose_on, ex_on, grp, np.abs(sec.r - py.r))

@@ -2,7 +2,7 @@
 # One GPU call that runs a list of steps in order, each under its own time limit, and stops
 # at the first step that fails, times out or crashes (no GPU work after a fault).
 #   bash tools/gpu_session.sh TAG step [step ...]
-# steps: resident | profile | nlab | suite | bench | benchsize
+# steps: resident | profile | nlab | suite | bench | bench_t2 | benchsize | trace | trace_c1
 set -u
 TAG=$1
 shift
@@ -27,9 +27,12 @@ for step in "$@"; do
     profile) run profile 300 python -u tools/ge_resident_profile.py ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
+    rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
     suite) run suite 1000 $PYT -m gpu tests ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
     bench_t2) run bench_t2 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    trace) export TMPDIR=/tmp; run trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --legs table2 ;;
+    trace_c1) export TMPDIR=/tmp; run trace_c1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
