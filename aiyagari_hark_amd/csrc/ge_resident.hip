@@ -76,6 +76,13 @@ struct GeRun {
   int* span;              // [n_cal][G][SMAX][4]
   unsigned* ctr;          // [n_cal][kHcCtrStride]
   unsigned long long* gran;   // [n_cal][2][G][kHcRedRec]
+  int pc_per, pc_builds;  // two-level preconditioner of the distribution solves (pc_per 0: off)
+  double pc_drop;
+  double* wg;             // [n_cal][S][n_a] prolongation weights
+  double* tc;             // [n_cal][nc][nc] coarse chain
+  double* mc;             // [n_cal][nc] aggregate masses
+  double* bi;             // [n_cal][G][per][nc] rows of the coarse inverse
+  unsigned long long* agran;   // [n_cal][2][G][2 kPcPer] all-gather granules
   unsigned* err;
   double* out_r;
   double* out_K;
@@ -661,7 +668,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     int mv;
     {
       HkArgs hk;
-      hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
+      hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1; hk.nj = g.nj;
       hk.LO = to_global((const int*)LO); hk.WL = to_global((const double*)WL); hk.X = to_global(X);
       hk.Pg = to_global(g.pg + row0); hk.Vg = to_global((double*)nullptr);
       hk.slab_cl = to_global(g.slab + (size_t)cal * G * 2 * g.cap);
@@ -669,7 +676,17 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
       hk.ctr = to_global(ctr); hk.gran = to_global(gran); hk.Pc = to_global(g.P + (size_t)cal * S * S);
       hk.max_iter = g.max_hist; hk.err = to_global(g.err);
       hk.tol = st.htol;
-      mv = hk_solve_isolated<SMAX, KC, TH>(hk, &nb, &ne);
+      const int nc = G * g.pc_per;
+      hk.pc_per = g.pc_per;
+      hk.pc_builds = g.pc_builds;
+      hk.pc_drop = g.pc_drop;
+      hk.Wg = to_global(g.wg + row0);
+      hk.Tc = to_global(g.tc + (size_t)cal * nc * nc);
+      hk.Mc = to_global(g.mc + (size_t)cal * nc);
+      hk.Bi = to_global(g.bi + (size_t)cal * G * g.pc_per * nc);
+      hk.agran = to_global(g.agran + (size_t)cal * 2 * G * 2 * kPcPer);
+      mv = g.pc_per > 0 ? hk_solve_isolated<SMAX, KC, TH, true>(hk, &nb, &ne)
+                        : hk_solve_isolated<SMAX, KC, TH, false>(hk, &nb, &ne);
     }
     if (mv < 0) return;
     if (tid == 0) {
@@ -728,7 +745,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
 // host side
 // ------------------------------------------------------------------------------------
 struct GePlan {
-  int G = 0, nj = 0, kc = 0, smax = 0, sc = 0, cap = 0, blocks = 0;
+  int G = 0, nj = 0, kc = 0, smax = 0, sc = 0, cap = 0, blocks = 0, per = 0;
   size_t lds = 0;
   const void* fn = nullptr;
 };
@@ -772,13 +789,29 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   if (p.lds < kGeEgmLds || p.lds <= vbytes + 4096) return false;
   p.cap = (int)((p.lds - vbytes) / sizeof(double));
   p.blocks = (p.G * n_cal + 7) / 8 * 8;
+  // two-level preconditioner: aggregates of >= 32 columns, at most kPcNc coarse unknowns, and
+  // the coarse build's scratch (column block + staged state; the fp32 Gauss-Jordan
+  // [nc][nc + per + 1] with its pivot row and column) within the dynamic LDS
+  p.per = 0;
+  if (h->hist_precond > 0) {
+    const int len_last = n_a - (p.G - 1) * p.nj;
+    int per = std::min(std::min(kPcPer, kPcNc / p.G), std::max(1, std::min(p.nj, len_last) / 32));
+    for (; per >= 1; --per) {
+      const size_t nc = (size_t)p.G * per;
+      const size_t gj = (nc * (nc + per + 1) + 3 * nc + 2 * per) * sizeof(float);
+      const size_t stage = nc * per * sizeof(double) + (size_t)p.nj * 20;
+      if (gj <= p.lds && stage <= p.lds) break;
+    }
+    p.per = per;
+  }
   return true;
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, prof, run, bytes;
+  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, wg, tc, mc, bi, agran, err, cal, outd, outi, prof, run,
+      bytes;
 };
-static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
+static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap, int per) {
   GeScratch L;
   size_t o = 0;
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
@@ -790,6 +823,12 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
   L.span = take((size_t)n_cal * G * 8 * 4 * sizeof(int));
   L.ctr = take((size_t)n_cal * kHcCtrStride * sizeof(unsigned));
   L.gran = take((size_t)n_cal * 2 * G * kHcRedRec * sizeof(unsigned long long));
+  const size_t nc = (size_t)G * per;
+  L.wg = take(per > 0 ? pts * 8 : 0);
+  L.tc = take((size_t)n_cal * nc * nc * sizeof(double));
+  L.mc = take((size_t)n_cal * nc * sizeof(double));
+  L.bi = take((size_t)n_cal * G * per * nc * sizeof(double));
+  L.agran = take((size_t)n_cal * 2 * G * 2 * kPcPer * sizeof(unsigned long long));
   L.err = take(256);
   L.cal = take((size_t)n_cal * sizeof(GeCalDev));
   L.outd = take((size_t)n_cal * 3 * sizeof(double));
@@ -818,7 +857,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
     (void)hipGetLastError();
     return 0;
   }
-  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap);
+  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap, p.per);
   if (L.bytes > h->ge_cap) {
     if (h->d_ge) (void)hipFree(h->d_ge);
     h->d_ge = nullptr;
@@ -855,6 +894,14 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.span = reinterpret_cast<int*>(base + L.span);
   g.ctr = reinterpret_cast<unsigned*>(base + L.ctr);
   g.gran = reinterpret_cast<unsigned long long*>(base + L.gran);
+  g.pc_per = p.per;
+  g.pc_builds = h->hist_precond;
+  g.pc_drop = 1e-2;
+  g.wg = reinterpret_cast<double*>(base + L.wg);
+  g.tc = reinterpret_cast<double*>(base + L.tc);
+  g.mc = reinterpret_cast<double*>(base + L.mc);
+  g.bi = reinterpret_cast<double*>(base + L.bi);
+  g.agran = reinterpret_cast<unsigned long long*>(base + L.agran);
   g.err = reinterpret_cast<unsigned*>(base + L.err);
   double* outd = reinterpret_cast<double*>(base + L.outd);
   int* outi = reinterpret_cast<int*>(base + L.outi);
@@ -865,6 +912,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n_cal * kHcCtrStride * sizeof(unsigned), st));
   AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n_cal * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
   AIY_HIP(h, hipMemsetAsync(g.err, 0, 256, st));
+  AIY_HIP(h, hipMemsetAsync(g.agran, 0, (size_t)n_cal * 2 * p.G * 2 * kPcPer * sizeof(unsigned long long), st));
   for (hipEvent_t& e : h->ge_ev)
     if (!e) AIY_HIP(h, hipEventCreate(&e));
   void* args[] = {&g};
