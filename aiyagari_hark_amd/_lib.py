@@ -37,7 +37,6 @@ AIY_OPT_HIST_ACCEL = 8
 AIY_OPT_HIST_KRYLOV = 9
 AIY_OPT_GE_RESIDENT = 10
 AIY_OPT_CU_LIMIT = 11
-AIY_OPT_HIST_PRECOND = 12
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

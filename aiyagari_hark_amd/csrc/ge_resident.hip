@@ -43,12 +43,18 @@
 
 namespace aiy {
 
-constexpr int kGeTH = 512;
-constexpr int kGeWaves = kGeTH / kWave;   // 8
+// Workgroup size (template TH; the plan launches 512).  A cycle / matvec costs about the same
+// per column of a workgroup whatever the thread organisation: 26.8 / 23.7 us at G = 10
+// (1 000 columns, 512 threads x 2 columns), 23.0 / 25.5 us with 1 024 threads x 1 column
+// (spills at 128 VGPRs), 15.5 / 12.4 us at G = 21 (477 columns, 512 threads x 1 column)
+// (profiles/r03i_*, r03j_*): a cluster's time scales with its columns per CU.
+constexpr int kGeTHMax = 1024;
+constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
 constexpr int kGeExtrap = 32;             // cycles between extrapolation checks (ge.hip's host chunk)
-constexpr size_t kGeEgmLds = (size_t)kGeWaves * (8 * kTile + 4 * kWin) * sizeof(double);   // V tiles + windows
+template <int NW>
+constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
 
 struct GeCalDev {
   double alpha, delta, disc, r_lo, r_hi;
@@ -76,13 +82,6 @@ struct GeRun {
   int* span;              // [n_cal][G][SMAX][4]
   unsigned* ctr;          // [n_cal][kHcCtrStride]
   unsigned long long* gran;   // [n_cal][2][G][kHcRedRec]
-  int pc_per, pc_builds;  // two-level preconditioner of the distribution solves (pc_per 0: off)
-  double pc_drop;
-  double* wg;             // [n_cal][S][n_a] prolongation weights
-  double* tc;             // [n_cal][nc][nc] coarse chain
-  double* mc;             // [n_cal][nc] aggregate masses
-  double* bi;             // [n_cal][G][per][nc] rows of the coarse inverse
-  unsigned long long* agran;   // [n_cal][2][G][2 kPcPer] all-gather granules
   unsigned* err;
   double* out_r;
   double* out_K;
@@ -115,7 +114,7 @@ struct GeState {
 // workgroup has published after all its waves drained their stores.
 template <int TH>
 __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w, unsigned& ne, const double* vals,
-                                          int nv, unsigned kmax, double (*s_part)[TH / kWave], double* s_res,
+                                          int nv, unsigned kmax, double (*s_part)[kGeWavesMax], double* s_res,
                                           int* s_flag, unsigned* err) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -185,7 +184,7 @@ __device__ __forceinline__ bool ge_reduce(unsigned long long* gran, int G, int w
 // hist_bicg.h column of the same thread): for every row s of `src` (S rows of n_a + 1
 // nodes) the HARK LinearInterp at q = R a_j + Wl[s], by the window search of egm.hip over
 // agent-scope loads; sink(tile, lane column, s, q, value) takes the result.
-template <int SMAX, typename Sink, typename Begin, typename End>
+template <int SMAX, int NW, typename Sink, typename Begin, typename End>
 __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, const double* __restrict__ a_grid,
                                              const double* __restrict__ src_m, const double* __restrict__ src_c,
                                              double R, const double* s_Wl, int* s_hint, double* lds_win,
@@ -199,7 +198,7 @@ __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, con
   double* XB = X + 2 * kWin;
   double* YB = X + 3 * kWin;
 #pragma unroll 1
-  for (int tile = wv; tile < ntile; tile += kGeWaves) {
+  for (int tile = wv; tile < ntile; tile += NW) {
     const int jr = j0 + tile * kTile + lane;
     const int j = jr < j1 ? jr : j1 - 1;   // lanes past the range repeat the last column
     const double a = a_grid[j];
@@ -263,7 +262,7 @@ __device__ __forceinline__ void ge_rows_pass(int S, int n_a, int j0, int j1, con
 
 // One EGM cycle of the workgroup's own nodes: src (cycle n - 1; nullptr: the terminal
 // c = m) -> dst (cycle n).  Returns the workgroup's part of the HARK distance (track).
-template <int SMAX, int SC, int PK>
+template <int SMAX, int SC, int PK, int NW>
 __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, const double* __restrict__ a_grid,
                                                const double* src_m, const double* src_c, double* dst_m,
                                                double* dst_c, bool track, double R, double beta, double gam,
@@ -277,7 +276,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
   double dmax = 0.0;
   if (src_m == nullptr) {   // terminal guess: IdentityFunction (AS:898) of mNextArray
 #pragma unroll 1
-    for (int tile = wv; tile < ntile; tile += kGeWaves) {
+    for (int tile = wv; tile < ntile; tile += NW) {
       const int jr = j0 + tile * kTile + lane;
       const int j = jr < j1 ? jr : j1 - 1;
       const double a = a_grid[j];
@@ -337,7 +336,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
       }
     }
   };
-  ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, src_m, src_c, R, s_Wl, s_hint, lds_win,
+  ge_rows_pass<SMAX, NW>(S, n_a, j0, j1, a_grid, src_m, src_c, R, s_Wl, s_hint, lds_win,
                      [&](int, int, int, int sp, double, double f) {
                        Vw[sp * kTile + lane] = R * marg_u<PK>(f, gam);   // RnextArray * MargValueFuncCRRA
                      },
@@ -349,7 +348,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
 // own non-inlined functions, each with its own register allocation) address it directly.
 constexpr int kGeSmax = 8;
 extern __shared__ double ge_dyn[];                 // histogram: span buffer + v; EGM: V tiles + windows
-__shared__ double ge_s_part[kHkRed][kGeWaves];
+__shared__ double ge_s_part[kHkRed][kGeWavesMax];
 __shared__ double ge_s_res[kHkRed];
 __shared__ int ge_s_flag;
 __shared__ double ge_s_Pe[kGeSmax * kGeSmax];     // P[s][s'] unpadded (egm_phase2's layout)
@@ -358,19 +357,19 @@ __shared__ int ge_s_hint[kGeMaxTiles * kGeSmax];  // window hints per (tile, row
 __shared__ unsigned ge_s_nc;
 __shared__ GeState ge_st;
 
-template <int SMAX, int SC, int PK>
+template <int SMAX, int SC, int PK, int NW>
 __device__ __forceinline__ double ge_egm_cycle_fn(int S, int n_a, int j0, int j1, const double* a_grid,
                                                const double* src_m, const double* src_c, double* dst_m,
                                                double* dst_c, bool track, double R, double beta, double gam) {
-  return ge_egm_cycle<SMAX, SC, PK>(S, n_a, j0, j1, a_grid, src_m, src_c, dst_m, dst_c, track, R, beta, gam, ge_s_Wl,
-                                    ge_s_Pe, ge_s_hint, ge_dyn, ge_dyn + (size_t)kGeWaves * SMAX * kTile);
+  return ge_egm_cycle<SMAX, SC, PK, NW>(S, n_a, j0, j1, a_grid, src_m, src_c, dst_m, dst_c, track, R, beta, gam,
+                                        ge_s_Wl, ge_s_Pe, ge_s_hint, ge_dyn, ge_dyn + (size_t)NW * SMAX * kTile);
 }
 
 // lottery of the own columns on the final tables (hist.hip hist_lottery_kernel's arithmetic)
-template <int SMAX>
+template <int SMAX, int NW>
 __device__ __forceinline__ void ge_lottery_fn(int S, int n_a, int j0, int j1, const double* a_grid, const double* fm,
                                            const double* fc, double R, bool have_prev, int* LO, double* WL) {
-  ge_rows_pass<SMAX>(S, n_a, j0, j1, a_grid, fm, fc, R, ge_s_Wl, ge_s_hint, ge_dyn + (size_t)kGeWaves * SMAX * kTile,
+  ge_rows_pass<SMAX, NW>(S, n_a, j0, j1, a_grid, fm, fc, R, ge_s_Wl, ge_s_hint, ge_dyn + (size_t)NW * SMAX * kTile,
                      [&](int, int jr, int, int s, double q, double c) {
                        if (jr >= j1) return;
                        const double ap = q - c;
@@ -397,12 +396,12 @@ __device__ __forceinline__ void ge_lottery_fn(int S, int n_a, int j0, int j1, co
                      [](int, int) {}, [](int, int, double) {});
 }
 
-template <int SMAX, int SC, int KC>
-__global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
-  constexpr int TH = kGeTH;
+template <int SMAX, int SC, int KC, int TH>
+__global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
+  constexpr int NW = TH / kWave;
   static_assert(SMAX <= kGeSmax, "file-scope LDS sized for 8 states");
   GeState& st = ge_st;
-  double (*s_part)[TH / kWave] = ge_s_part;
+  double (*s_part)[kGeWavesMax] = ge_s_part;
   double* s_res = ge_s_res;
   int& s_flag = ge_s_flag;
   double* s_Pe = ge_s_Pe;
@@ -528,16 +527,16 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
         const bool track = n >= 2;
         double dl;
         if (pk == 1)
-          dl = ge_egm_cycle_fn<SMAX, SC, 1>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+          dl = ge_egm_cycle_fn<SMAX, SC, 1, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
                                             gam);
         else if (pk == 3)
-          dl = ge_egm_cycle_fn<SMAX, SC, 3>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+          dl = ge_egm_cycle_fn<SMAX, SC, 3, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
                                             gam);
         else if (pk == 5)
-          dl = ge_egm_cycle_fn<SMAX, SC, 5>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+          dl = ge_egm_cycle_fn<SMAX, SC, 5, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
                                             gam);
         else
-          dl = ge_egm_cycle_fn<SMAX, SC, 0>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+          dl = ge_egm_cycle_fn<SMAX, SC, 0, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
                                             gam);
         // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
         // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
@@ -643,7 +642,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     __syncthreads();
     // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
     tp = __builtin_amdgcn_s_memrealtime();
-    ge_lottery_fn<SMAX>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
+    ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
     // ---- the distribution's start (own columns) ----
     if (st.fresh_mass) {
       const double u0 = 1.0 / ((double)S * n_a);
@@ -668,7 +667,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
     int mv;
     {
       HkArgs hk;
-      hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1; hk.nj = g.nj;
+      hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
       hk.LO = to_global((const int*)LO); hk.WL = to_global((const double*)WL); hk.X = to_global(X);
       hk.Pg = to_global(g.pg + row0); hk.Vg = to_global((double*)nullptr);
       hk.slab_cl = to_global(g.slab + (size_t)cal * G * 2 * g.cap);
@@ -676,17 +675,7 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
       hk.ctr = to_global(ctr); hk.gran = to_global(gran); hk.Pc = to_global(g.P + (size_t)cal * S * S);
       hk.max_iter = g.max_hist; hk.err = to_global(g.err);
       hk.tol = st.htol;
-      const int nc = G * g.pc_per;
-      hk.pc_per = g.pc_per;
-      hk.pc_builds = g.pc_builds;
-      hk.pc_drop = g.pc_drop;
-      hk.Wg = to_global(g.wg + row0);
-      hk.Tc = to_global(g.tc + (size_t)cal * nc * nc);
-      hk.Mc = to_global(g.mc + (size_t)cal * nc);
-      hk.Bi = to_global(g.bi + (size_t)cal * G * g.pc_per * nc);
-      hk.agran = to_global(g.agran + (size_t)cal * 2 * G * 2 * kPcPer);
-      mv = g.pc_per > 0 ? hk_solve_isolated<SMAX, KC, TH, true>(hk, &nb, &ne)
-                        : hk_solve_isolated<SMAX, KC, TH, false>(hk, &nb, &ne);
+      mv = hk_solve_isolated<SMAX, KC, TH>(hk, &nb, &ne);
     }
     if (mv < 0) return;
     if (tid == 0) {
@@ -745,14 +734,14 @@ __global__ __launch_bounds__(kGeTH) void ge_cluster_kernel(GeRun g) {
 // host side
 // ------------------------------------------------------------------------------------
 struct GePlan {
-  int G = 0, nj = 0, kc = 0, smax = 0, sc = 0, cap = 0, blocks = 0, per = 0;
+  int G = 0, nj = 0, kc = 0, smax = 0, sc = 0, cap = 0, blocks = 0, th = 0;
   size_t lds = 0;
   const void* fn = nullptr;
 };
 
-template <int SMAX, int SC, int KC>
+template <int SMAX, int SC, int KC, int TH>
 static const void* ge_fn() {
-  return reinterpret_cast<const void*>(ge_cluster_kernel<SMAX, SC, KC>);
+  return reinterpret_cast<const void*>(ge_cluster_kernel<SMAX, SC, KC, TH>);
 }
 
 // Launch shape of the device-resident search for (n_cal, S, n_a): every calibration's
@@ -762,8 +751,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
-  const int th = kGeTH;
-  const int g_min = (n_a + 2 * th - 1) / (2 * th);
+  const int g_min = (n_a + 2 * 512 - 1) / (2 * 512);
   const int g_cap = h->hist_cluster_cap > 0 ? h->hist_cluster_cap : 32;
   int G = std::max(g_min, std::min(std::min(g_cap, kHcMaxG), cus / n_cal));
   G = std::min(G, n_a);
@@ -771,11 +759,13 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   p.G = (n_a + p.nj - 1) / p.nj;
   if (p.nj > kGeMaxTiles * kTile) return false;
   if ((long long)p.G * n_cal > cus) return false;
+  p.th = 512;
+  const int th = p.th;
   p.kc = p.nj <= th ? 1 : 2;
   p.smax = S == 7 ? 7 : 8;   // the Table II shape: exact state count (fewer registers in the solve)
   p.sc = S == 7 ? 7 : 0;
-  if (p.sc == 7) p.fn = p.kc == 1 ? ge_fn<7, 7, 1>() : ge_fn<7, 7, 2>();
-  else p.fn = p.kc == 1 ? ge_fn<8, 0, 1>() : ge_fn<8, 0, 2>();
+  if (p.sc == 7) p.fn = p.kc == 1 ? ge_fn<7, 7, 1, 512>() : ge_fn<7, 7, 2, 512>();
+  else p.fn = p.kc == 1 ? ge_fn<8, 0, 1, 512>() : ge_fn<8, 0, 2, 512>();
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
   int lds_dev = 0;
@@ -786,32 +776,17 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   if (stat + 4096 >= lds_total) return false;
   p.lds = (lds_total - stat - 1024) / 256 * 256;
   const size_t vbytes = (size_t)p.kc * p.smax * th * sizeof(double);   // BiCGSTAB v behind the spans
-  if (p.lds < kGeEgmLds || p.lds <= vbytes + 4096) return false;
+  const size_t egm_lds = ge_egm_lds<8>();
+  if (p.lds < egm_lds || p.lds <= vbytes + 4096) return false;
   p.cap = (int)((p.lds - vbytes) / sizeof(double));
   p.blocks = (p.G * n_cal + 7) / 8 * 8;
-  // two-level preconditioner: aggregates of >= 32 columns, at most kPcNc coarse unknowns, and
-  // the coarse build's scratch (column block + staged state; the fp32 Gauss-Jordan
-  // [nc][nc + per + 1] with its pivot row and column) within the dynamic LDS
-  p.per = 0;
-  if (h->hist_precond > 0) {
-    const int len_last = n_a - (p.G - 1) * p.nj;
-    int per = std::min(std::min(kPcPer, kPcNc / p.G), std::max(1, std::min(p.nj, len_last) / 32));
-    for (; per >= 1; --per) {
-      const size_t nc = (size_t)p.G * per;
-      const size_t gj = (nc * (nc + per + 1) + 3 * nc + 2 * per) * sizeof(float);
-      const size_t stage = nc * per * sizeof(double) + (size_t)p.nj * 20;
-      if (gj <= p.lds && stage <= p.lds) break;
-    }
-    p.per = per;
-  }
   return true;
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, wg, tc, mc, bi, agran, err, cal, outd, outi, prof, run,
-      bytes;
+  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, prof, run, bytes;
 };
-static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap, int per) {
+static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
   GeScratch L;
   size_t o = 0;
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
@@ -823,12 +798,6 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap, in
   L.span = take((size_t)n_cal * G * 8 * 4 * sizeof(int));
   L.ctr = take((size_t)n_cal * kHcCtrStride * sizeof(unsigned));
   L.gran = take((size_t)n_cal * 2 * G * kHcRedRec * sizeof(unsigned long long));
-  const size_t nc = (size_t)G * per;
-  L.wg = take(per > 0 ? pts * 8 : 0);
-  L.tc = take((size_t)n_cal * nc * nc * sizeof(double));
-  L.mc = take((size_t)n_cal * nc * sizeof(double));
-  L.bi = take((size_t)n_cal * G * per * nc * sizeof(double));
-  L.agran = take((size_t)n_cal * 2 * G * 2 * kPcPer * sizeof(unsigned long long));
   L.err = take(256);
   L.cal = take((size_t)n_cal * sizeof(GeCalDev));
   L.outd = take((size_t)n_cal * 3 * sizeof(double));
@@ -853,11 +822,11 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
     return 0;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, kGeTH, p.lds) != hipSuccess || per_cu < 1) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds) != hipSuccess || per_cu < 1) {
     (void)hipGetLastError();
     return 0;
   }
-  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap, p.per);
+  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap);
   if (L.bytes > h->ge_cap) {
     if (h->d_ge) (void)hipFree(h->d_ge);
     h->d_ge = nullptr;
@@ -894,14 +863,6 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.span = reinterpret_cast<int*>(base + L.span);
   g.ctr = reinterpret_cast<unsigned*>(base + L.ctr);
   g.gran = reinterpret_cast<unsigned long long*>(base + L.gran);
-  g.pc_per = p.per;
-  g.pc_builds = h->hist_precond;
-  g.pc_drop = 1e-2;
-  g.wg = reinterpret_cast<double*>(base + L.wg);
-  g.tc = reinterpret_cast<double*>(base + L.tc);
-  g.mc = reinterpret_cast<double*>(base + L.mc);
-  g.bi = reinterpret_cast<double*>(base + L.bi);
-  g.agran = reinterpret_cast<unsigned long long*>(base + L.agran);
   g.err = reinterpret_cast<unsigned*>(base + L.err);
   double* outd = reinterpret_cast<double*>(base + L.outd);
   int* outi = reinterpret_cast<int*>(base + L.outi);
@@ -912,12 +873,11 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n_cal * kHcCtrStride * sizeof(unsigned), st));
   AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n_cal * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
   AIY_HIP(h, hipMemsetAsync(g.err, 0, 256, st));
-  AIY_HIP(h, hipMemsetAsync(g.agran, 0, (size_t)n_cal * 2 * p.G * 2 * kPcPer * sizeof(unsigned long long), st));
   for (hipEvent_t& e : h->ge_ev)
     if (!e) AIY_HIP(h, hipEventCreate(&e));
   void* args[] = {&g};
   AIY_HIP(h, hipEventRecord(h->ge_ev[0], st));
-  AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(kGeTH), args, p.lds, st));
+  AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(p.th), args, p.lds, st));
   AIY_HIP(h, hipEventRecord(h->ge_ev[1], st));
   std::vector<double> hd(3 * (size_t)n_cal);
   std::vector<int> hi(4 * (size_t)n_cal);

@@ -12,11 +12,6 @@ namespace aiy {
 constexpr int kHkRed = 8;   // partial sums per reduction (at most)
 constexpr int kHkStall = 256;   // matvecs without a 10 % residual gain that count as a stall
 static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
-// two-level (aggregation) preconditioner of the Krylov solve: contiguous asset intervals of
-// each workgroup's own columns, the same for every income state
-constexpr int kPcPer = 16;    // aggregates per workgroup (at most)
-constexpr int kPcNc = 160;    // coarse unknowns (at most)
-constexpr double kPcDelta = 1e-280;   // weight floor: a massless aggregate gets uniform weights
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
 __device__ __forceinline__ double hk_rhat(unsigned q) {
@@ -62,30 +57,7 @@ struct HkShared {
   double* s_res;                   // [kHkRed]
   int* s_flag;
   int* s_stop;
-  double* s_b;                     // [kPcNc] all-gathered restriction R q
-  double (*s_Y)[kPcPer];           // [8][kPcPer] coarse coefficients (own aggregates)
-  double (*s_seg)[TH / kWave][3];  // [KC][waves][3] segmented aggregate sums
-  int* s_misc;                     // [4]
 };
-
-// The LDS of one solve (static part), declared by each kernel that runs hk_solve.
-#define AIY_HK_SHARED(SMAX, KC, TH, dyn)                                                        \
-  __shared__ int s_base[SMAX];                                                                 \
-  __shared__ int s_pub[2 * SMAX][2];                                                           \
-  __shared__ int s_tot;                                                                        \
-  __shared__ HcCand s_cand[SMAX][kHcCand];                                                     \
-  __shared__ int s_ncand[SMAX];                                                                \
-  __shared__ unsigned short s_cinfo[KC * SMAX * TH];                                           \
-  __shared__ double s_P[SMAX * SMAX];                                                          \
-  __shared__ double s_part[kHkRed][TH / kWave];                                                \
-  __shared__ double s_res[kHkRed];                                                             \
-  __shared__ int s_flag, s_stop;                                                               \
-  __shared__ double s_b[kPcNc];                                                                \
-  __shared__ double s_Y[8][kPcPer];                                                            \
-  __shared__ double s_seg[KC][TH / kWave][3];                                                  \
-  __shared__ int s_misc[4];                                                                    \
-  const HkShared<SMAX, KC, TH> L{dyn,   s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, \
-                                 s_part, s_res, &s_flag, &s_stop, s_b, s_Y, s_seg, s_misc}
 
 // One calibration's BiCGSTAB distribution solve by the workgroups of its cluster (this
 // workgroup: w of G, own columns [j0, j1)); shared by hist_bicg_kernel (one solve per
@@ -93,7 +65,7 @@ struct HkShared {
 // (pointers typed global: hk_solve_isolated receives them as plain arguments, where the
 // compiler could not infer their address space and would use flat accesses)
 struct HkArgs {
-  int G, S, n_a, cap, w, j0, j1, nj;   // nj: the cluster's column stride (workgroup w owns [w nj, (w + 1) nj))
+  int G, S, n_a, cap, w, j0, j1;
   gptr<const int> LO;          // [S][n_a] lottery of the calibration (index)
   gptr<const double> WL;       // [S][n_a] lottery weight on lo
   gptr<double> X;              // [S][n_a] in: start, out: T x (own columns)
@@ -107,217 +79,12 @@ struct HkArgs {
   double tol;
   int max_iter;
   gptr<unsigned> err;
-  // two-level preconditioner (pc_per == 0: plain BiCGSTAB)
-  int pc_per;                  // aggregates per workgroup
-  int pc_builds;               // coarse operators built per solve (at most)
-  double pc_drop;              // rebuild (and restart) once the residual fell by this factor
-  gptr<double> Wg;             // [S][n_a] prolongation weights (own columns)
-  gptr<double> Tc;             // [nc][nc] coarse chain T_c[J][I] (cluster)
-  gptr<double> Mc;             // [nc] aggregate masses (cluster)
-  gptr<double> Bi;             // [G][per][nc] each workgroup's rows of the coarse inverse
-  gptr<unsigned long long> agran;   // [2][G][2 kPcPer] all-gather granules
 };
-
-// build the coarse operator from the current iterate x (in X): weights W = (x+ + delta) /
-// (aggregate mass), the coarse chain T_c[J][I] = sum over I's points of W (wlo [agg(lo) = J]
-// + (1 - wlo) [agg(lo + 1) = J]) (the income mix drops out: every state shares the
-// aggregates), Ac~ = I - T_c with the row of the heaviest aggregate k* replaced by ones;
-// each workgroup inverts Ac~^T against its own unit columns (Gauss-Jordan, fp32: it only
-// preconditions) and keeps its rows of Ac~^-1 with column k* zeroed.  Uses the span
-// buffer as scratch and leaves it zeroed.
-// (its own function: the Gauss-Jordan and the ordered walks must not add to the solve's
-// register pressure; nothing of the solve is live across the call)
-template <int SMAX, int KC, int TH>
-__device__ __noinline__ bool hk_pc_build(HkArgs r, HkShared<SMAX, KC, TH> L, unsigned* nb_io) {
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const int G = r.G, S = r.S, n_a = r.n_a, w = r.w, j0 = r.j0, j1 = r.j1, nj = r.nj;
-  const int per = r.pc_per, nc = G * per, len = j1 - j0;
-  double* Tacc = L.Tacc;
-  double (*s_Y)[kPcPer] = L.s_Y;
-  const int s_tot = *L.s_tot;
-  const double* X = (const double*)r.X;
-  const int* LO = (const int*)r.LO;
-  const double* WL = (const double*)r.WL;
-  int akc[KC];
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const int c = tid + k * TH;
-    akc[k] = c < len ? (c * per) / len : 0;
-  }
-  auto col = [&]() { return j0 + tid; };
-  auto barrier = [&]() -> bool {
-    ++*nb_io;
-    return hc_barrier((unsigned*)r.err, (unsigned*)r.ctr, (unsigned)G * *nb_io, L.s_flag);
-  };
-  auto agg_of = [&](int d) {
-    const int w2 = d / nj, c2 = d - w2 * nj, l2 = min(nj, n_a - w2 * nj);
-    return w2 * per + (c2 * per) / l2;
-  };
-  auto agg_end = [&](int J) {
-    const int w2 = J / per, a2 = J - w2 * per, l2 = min(nj, n_a - w2 * nj);
-    return w2 * nj + ((a2 + 1) * l2 + per - 1) / per;
-  };
-  double* Cb = Tacc;                    // [nc][per] own columns of T_c (unnormalised)
-  double* stx = Tacc + nc * per;        // staged own columns of one state: x, wlo, lo
-  double* stw = stx + len;
-  int* stl = reinterpret_cast<int*>(stw + len);
-  for (int q = tid; q < nc * per; q += TH) Cb[q] = 0.0;
-  double msum = 0.0;
-  __syncthreads();
-  for (int s = 0; s < S; ++s) {
-    for (int c = tid; c < len; c += TH) {
-      const size_t g = (size_t)s * n_a + j0 + c;
-      stx[c] = X[g];
-      stw[c] = WL[g];
-      stl[c] = LO[g];
-    }
-    __syncthreads();
-    if (tid < per) {   // one thread per own aggregate, its columns in order (deterministic)
-      const int i = tid;
-      const int cb = (i * len + per - 1) / per, ce = ((i + 1) * len + per - 1) / per;
-      int J = -1, endJ = -1;
-      for (int c = cb; c < ce; ++c) {
-        const double xv = fmax(stx[c], 0.0) + kPcDelta;
-        const int d = stl[c];
-        const double wl = stw[c];
-        if (J < 0 || d >= endJ) {
-          J = agg_of(d);
-          endJ = agg_end(J);
-        }
-        Cb[J * per + i] += xv * wl;
-        Cb[(d + 1 >= endJ ? J + 1 : J) * per + i] += xv * (1.0 - wl);
-        msum += xv;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid < per) s_Y[7][tid] = msum;
-  __syncthreads();
-  double* Tc = (double*)r.Tc;
-  double* Mc = (double*)r.Mc;
-  double* Wgw = (double*)r.Wg;
-  {
-    const int jc = col();
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      const double im = 1.0 / s_Y[7][akc[k]];
-      for (int s = 0; s < S; ++s)
-        if (jc + k * TH < j1) {
-          const size_t g = (size_t)s * n_a + jc + k * TH;
-          Wgw[g] = (fmax(X[g], 0.0) + kPcDelta) * im;
-        }
-    }
-  }
-  for (int q = tid; q < nc * per; q += TH) {
-    const int J = q / per, i = q - J * per;
-    store_f64_agent(&Tc[(size_t)J * nc + w * per + i], Cb[q] / s_Y[7][i]);
-  }
-  if (tid < per) store_f64_agent(&Mc[w * per + tid], s_Y[7][tid]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (!barrier()) return false;
-  if (wid == 0) {   // k* = the heaviest aggregate (lowest index on ties), the same everywhere
-    double bm = -1.0;
-    int bk = 0;
-    for (int q = lane; q < nc; q += kWave) {
-      const double m = load_f64_agent(&Mc[q]);
-      if (m > bm) {
-        bm = m;
-        bk = q;
-      }
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double om = __shfl_xor(bm, o);
-      const int ok = __shfl_xor(bk, o);
-      if (om > bm || (om == bm && ok < bk)) {
-        bm = om;
-        bk = ok;
-      }
-    }
-    if (lane == 0) L.s_misc[0] = bk;
-  }
-  __syncthreads();
-  const int ks = L.s_misc[0];
-  const int ncol = nc + per, ld = ncol + 1;
-  float* A = reinterpret_cast<float*>(Tacc);
-  float* fcol = A + (size_t)nc * ld;
-  float* prow = fcol + nc;
-  auto pi = [&](int a) { return a == ks ? nc - 1 : (a == nc - 1 ? ks : a); };
-  for (int q = tid; q < nc * ncol; q += TH) {
-    const int a = q / ncol, b = q - a * ncol;
-    float v;
-    if (b < nc) {
-      const int I = pi(a), J = pi(b);
-      v = J == ks ? 1.0f : (float)((I == J ? 1.0 : 0.0) - load_f64_agent(&Tc[(size_t)J * nc + I]));
-    } else {
-      v = pi(a) == w * per + (b - nc) ? 1.0f : 0.0f;
-    }
-    A[(size_t)a * ld + b] = v;
-  }
-  __syncthreads();
-  // Gauss-Jordan with partial pivoting (row swaps leave the solution order alone); every
-  // workgroup runs the same pivot sequence on the same matrix (the unit columns do not
-  // enter the pivot choice), so a bad coarse operator is bad everywhere
-  const int ti = tid >> 5, tcl = tid & 31;
-  float* krow = prow + ncol;
-  for (int k = 0; k < nc; ++k) {
-    for (int q = tid; q < nc; q += TH) fcol[q] = A[(size_t)q * ld + k];
-    __syncthreads();
-    float bv = -1.0f;   // pivot row: max |A[i][k]| over i >= k (lowest index on ties), every wave
-    int bp = k;
-    for (int q = k + lane; q < nc; q += kWave) {
-      const float v = fabsf(fcol[q]);
-      if (v > bv) {
-        bv = v;
-        bp = q;
-      }
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ov = __shfl_xor(bv, o);
-      const int op = __shfl_xor(bp, o);
-      if (ov > bv || (ov == bv && op < bp)) {
-        bv = ov;
-        bp = op;
-      }
-    }
-    const int pr = bp;
-    for (int q = tid; q < ncol; q += TH) {
-      prow[q] = A[(size_t)pr * ld + q];
-      krow[q] = A[(size_t)k * ld + q];
-    }
-    __syncthreads();
-    float pv0 = fcol[pr];
-    if (!(fabsf(pv0) > 1e-30f)) pv0 = 1e-30f;   // singular coarse chain: finite garbage, caught below
-    const float ip = 1.0f / pv0;
-    for (int i = ti; i < nc; i += TH / 32) {
-      const float f = (i == pr ? fcol[k] : fcol[i]) * ip;   // row pr holds the old row k after the swap
-      for (int c = k + 1 + tcl; c < ncol; c += 32) {
-        const float old = i == pr ? krow[c] : A[(size_t)i * ld + c];
-        A[(size_t)i * ld + c] = i == k ? prow[c] * ip : old - f * prow[c];
-      }
-    }
-    __syncthreads();
-  }
-  double* bi = (double*)r.Bi + (size_t)w * per * nc;
-  bool bad = false;
-  for (int q = tid; q < per * nc; q += TH) {
-    const int i = q / nc, J = q - i * nc;
-    const double v = J == ks ? 0.0 : (double)A[(size_t)pi(J) * ld + nc + i];
-    bad = bad || !(fabs(v) < 1e12);
-    bi[q] = v;
-  }
-  if (tid == 0) L.s_misc[2] = 0;
-  __syncthreads();
-  if (bad) L.s_misc[2] = 1;
-  __syncthreads();
-  for (int q = tid; q < s_tot; q += TH) Tacc[q] = 0.0;   // the span buffer, as the matvec needs it
-  __syncthreads();
-  return true;
-}
 
 // Returns the matvecs of the solve, or -1 when the cluster stops (error word set: a
 // timeout, a span that does not fit, too many covering workgroups).  nb / ne: the
 // cluster barriers / reductions passed so far in this launch (counted on).
-template <int SMAX, int KC, int TH, bool PC = false>
+template <int SMAX, int KC, int TH>
 __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
                                         unsigned& ne) {
   constexpr bool kVlds = SMAX <= 8;
@@ -435,7 +202,9 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       s_cinfo[(k * SMAX + s) * TH + tid] = (unsigned short)(cf | (cn << 8));
     }
   }
-  constexpr bool kLoReg = SMAX <= 8 && KC == 1;   // with two columns per thread the registers hold the Krylov vectors
+  // lottery in registers with one column per thread at <= 8 waves (256 VGPRs); with two columns
+  // per thread, or 16 waves (128 VGPRs), the registers hold the Krylov vectors
+  constexpr bool kLoReg = SMAX <= 8 && KC == 1 && TH <= 512;
   int dreg[KC][kLoReg ? SMAX : 1];
   double wreg[KC][kLoReg ? SMAX : 1];
   if constexpr (kLoReg) {
@@ -640,23 +409,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     HK_PH(3);
     return true;
   };
-  // two-level preconditioner: aggregate a of local column c is (c per) / len, so each
-  // aggregate is a run of >= 32 columns (the host picks per <= len / 32) and a wave's 64
-  // columns touch at most three aggregates
-  const int per = r.pc_per;
-  bool pc = PC && per > 0;   // cleared for the rest of the solve when the coarse operator is unusable
-  const int nc = G * per;
-  const int len = j1 - j0;
-  const int nj = r.nj;
-  double* s_b = L.s_b;
-  double (*s_Y)[kPcPer] = L.s_Y;   // 0 Yr, 1 Yv, 2 Yt, 3 Yp, 4 Zp, 5 Yx, 6 Ys, 7 own aggregate sums
-  int akc[KC];
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const int c = tid + k * TH;
-    akc[k] = (pc && c < len) ? (c * per) / len : 0;
-  }
-
+  // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
+  // fixed order at every level, so every workgroup gets the same s_res
   // cluster-wide reduction of NV per-thread partials (bit v of kmax: nan_max, else sum),
   // fixed order at every level, so every workgroup gets the same s_res.  The workgroup's
   // values travel as tagged 8-byte granules ({epoch, 32 data bits}, two per double, sc1
@@ -665,9 +419,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   // every tag carries this reduction's epoch.  Epochs count up from 1 within a launch (the
   // host zeroes the granules before each launch); slots alternate by epoch parity, and a
   // matvec barrier separates any two reductions, so a slot is rewritten only after every
-  // workgroup has read it.  ag: also all-gather every workgroup's per aggregate sums
-  // (s_Y[7]) into s_b[nc] (the restriction R q of the preconditioner), same protocol.
-  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, bool ag, auto&& prefetch) -> bool {
+  // workgroup has read it.
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, auto&& prefetch) -> bool {
     HK_PH(5);
 #pragma unroll
     for (int v = 0; v < kHkRed; ++v) {
@@ -680,7 +433,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     ++ne;
     const unsigned long long tag = (unsigned long long)ne << 32;
     unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
-    unsigned long long* aslot = (unsigned long long*)r.agran + (size_t)(ne & 1) * G * (2 * kPcPer);
     if (tid < nv) {
       const int v = tid;
       double x = s_part[v][0];
@@ -689,16 +441,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       unsigned long long* g = slot + (size_t)w * (2 * kHkRed) + 2 * v;
       __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (ag && tid >= kWave && tid < kWave + per) {
-      const int i = tid - kWave;
-      const unsigned long long b = (unsigned long long)__double_as_longlong(s_Y[7][i]);
-      unsigned long long* g = aslot + (size_t)w * (2 * kPcPer) + 2 * i;
-      __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     prefetch();   // loads the step after the reduction needs, in flight across the sweep
     if (wid == 0) {
-      double xa[kHkRed], xb[kHkRed], xg[3];
+      double xa[kHkRed], xb[kHkRed];
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       bool ok;
       do {   // every granule load of a pass in flight before the tag test
@@ -720,21 +466,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             else xb[v] = x;
           }
         }
-        if (ag) {
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            const int q = lane + u * kWave;
-            xg[u] = 0.0;
-            if (q < nc) {
-              const int w2 = q / per, i = q - w2 * per;
-              const unsigned long long* g = aslot + (size_t)w2 * (2 * kPcPer) + 2 * i;
-              const unsigned long long hi = __hip_atomic_load(to_global(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              const unsigned long long lo = __hip_atomic_load(to_global(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
-              xg[u] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
-            }
-          }
-        }
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
@@ -751,82 +482,12 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           if (lane == kWave - 1) s_res[v] = y;
         }
       }
-      if (ag) {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int q = lane + u * kWave;
-          if (q < nc) s_b[q] = xg[u];
-        }
-      }
     }
     __syncthreads();
     HK_PH(4);
     return s_flag != 0;
   };
 
-  // ---- the two-level preconditioner M^-1 q = q + W o (Ac~^-1 R q)[agg] ----
-  // (right preconditioning: BiCGSTAB on (I - T) M^-1; x and the residuals stay those of the
-  // unpreconditioned system, so the stopping rule is unchanged)
-  // per-aggregate sums of the own column sums cs[k] into s_Y[7][0 .. per), fixed order
-  auto agg_sums = [&](const double (&cs)[KC]) {
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      const int c0 = wid * kWave + k * TH;   // the wave's first local column (wave-uniform)
-      double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-      if (c0 < len) {
-        const int a0 = (c0 * per) / len;
-        const int c = c0 + lane;
-        const int a = c < len ? akc[k] : -1;
-        x0 = wave_sum_lane63(a == a0 ? cs[k] : 0.0);
-        x1 = wave_sum_lane63(a == a0 + 1 ? cs[k] : 0.0);
-        x2 = wave_sum_lane63(a == a0 + 2 ? cs[k] : 0.0);
-      }
-      if (lane == kWave - 1) {
-        L.s_seg[k][wid][0] = x0;
-        L.s_seg[k][wid][1] = x1;
-        L.s_seg[k][wid][2] = x2;
-      }
-    }
-    __syncthreads();
-    if (tid < per) {
-      double sum = 0.0;
-      for (int k = 0; k < KC; ++k)
-        for (int wv = 0; wv < TH / kWave; ++wv) {
-          const int c0 = wv * kWave + k * TH;
-          if (c0 < len) {
-            const int q = tid - (c0 * per) / len;
-            if (q >= 0 && q < 3) sum += L.s_seg[k][wv][q];
-          }
-        }
-      s_Y[7][tid] = sum;
-    }
-    __syncthreads();
-  };
-  // the own aggregates' coarse coefficients s_Y[slot] = Bi_own s_b (s_b: the gathered R q)
-  auto coarse_y = [&](int slot) {
-    const double* bi = (const double*)r.Bi + (size_t)w * per * nc;
-    for (int i = wid; i < per; i += TH / kWave) {
-      double acc = 0.0;
-      for (int J = lane; J < nc; J += kWave) acc += bi[(size_t)i * nc + J] * s_b[J];
-      acc = wave_sum_lane63(acc);
-      if (lane == kWave - 1) s_Y[slot][i] = acc;
-    }
-    __syncthreads();
-  };
-  // q += sign W o s_Y[slot][agg] on the own points
-  const double* Wg = (const double*)r.Wg;
-  auto wadd = [&](double (&q)[KC][SMAX], int slot, double sign) {
-    const int jc = col();
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      const double y = sign * s_Y[slot][akc[k]];
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        const double wv = Wg[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
-        if (s < S && jc + k * TH < j1) q[k][s] += wv * y;
-      }
-    }
-  };
   // ---- BiCGSTAB ----
   // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
   // p in the HBM scratch row across the second matvec, whose gather needs the registers
@@ -847,35 +508,11 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   double best = __builtin_inf();   // best recursive max|r| since the last restart, and when
   int mv_best = 0;
   auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
-  // preconditioner: coarse operators built so far, a rebuild pending, the true residual at
-  // the last build.  Coarse coefficients (own aggregates, s_Y): Yr/Yv/Yt/Yp = Bi_own R of
-  // r/v/t/p; the matvec input p^ = pv + W Zp; x = X + W Yx (Yx folded into X at restarts).
-  int builds = 0;
-  bool rebuild = false, fresh = false;
-  double res_build = 0.0;
   HK_PH(-1);
   while (true) {
     if (restart) {
-      int jc = col();
-      if (builds > 0) {   // fold the coarse part of x (a no-op once the preconditioner is off)
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          const double y = s_Y[5][akc[k]];
-          for (int s = 0; s < S; ++s)
-            if (jc + k * TH < j1) X[gidx(jc, k, s)] += Wg[gidx(jc, k, s)] * y;
-        }
-        __syncthreads();
-        if (tid < per) s_Y[5][tid] = 0.0;
-        __syncthreads();
-      }
-      if (pc && (builds == 0 || rebuild)) {
-        if (!hk_pc_build<SMAX, KC, TH>(r, L, &nb)) return -1;
-        ++builds;
-        rebuild = false;
-        fresh = true;
-        jc = col();
-      }
       // true residual of x: pv = x, tv = T x, rv = T x - x
+      int jc = col();
 #pragma unroll
       for (int k = 0; k < KC; ++k)
 #pragma unroll
@@ -886,10 +523,9 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       if (!matvec(pv, tv)) return -1;
       ++mv;
       jc = col();
-      double rr = 0.0, rm = 0.0, xs = 0.0, cs[KC];
+      double rr = 0.0, rm = 0.0, xs = 0.0;
 #pragma unroll
-      for (int k = 0; k < KC; ++k) {
-        cs[k] = 0.0;
+      for (int k = 0; k < KC; ++k)
 #pragma unroll
         for (int s = 0; s < SMAX; ++s) {
           rv[k][s] = tv[k][s] - pv[k][s];
@@ -897,29 +533,12 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             rr += rh_at(jc, k, s) * rv[k][s];
             rm = nan_max(rm, fabs(rv[k][s]));
             xs += pv[k][s];
-            cs[k] += rv[k][s];
           }
         }
-      }
       part[0] = rr;
       part[1] = rm;
       part[2] = xs;
-      part[3] = pc ? (double)L.s_misc[2] : 0.0;   // a coarse inverse with non-finite / huge entries
-      if (pc) agg_sums(cs);
-      if (!reduce(part, 4, 10u, pc, [] {})) return -1;
-      if (pc && s_res[3] != 0.0) pc = false;   // the same decision in every workgroup
-      if (pc) {
-        coarse_y(0);
-#ifdef AIY_DIAG_PC
-        if (blockIdx.x == 0 && tid == 0 && mv < 400)
-          printf("[pc] restart mv=%d builds=%d rho=%.3e max|r|=%.3e sum=%.6e b0=%.3e b1=%.3e Yr0=%.3e Yr1=%.3e\n", mv,
-                 builds, s_res[0], s_res[1], s_res[2], s_b[0], s_b[1], s_Y[0][0], s_Y[0][per > 1 ? 1 : 0]);
-#endif
-        if (fresh) res_build = s_res[1];
-        fresh = false;
-        if (tid < per) s_Y[3][tid] = s_Y[4][tid] = s_Y[0][tid];   // p = r
-        __syncthreads();
-      }
+      if (!reduce(part, 3, 2u, [] {})) return -1;
       rho = s_res[0];
       if (mv == 1) total0 = s_res[2];   // the starting mass's total
       if (s_res[1] < tol || mv >= r.max_iter) {   // converged (np.max(...) < tol: NaN never is)
@@ -941,20 +560,18 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       restart = false;
       first = true;
     }
-    // v = p^ - T p^ (to LDS); alpha = rho / <rh, v>; the previous step's max|r| rides along.
-    // r waits in v's slot during this matvec (only p^ and the result stay in registers)
+    // v = p - T p (to LDS); alpha = rho / <rh, v>; the previous step's max|r| rides along.
+    // r waits in v's slot during this matvec (only p and the result stay in registers)
 #pragma unroll
     for (int k = 0; k < KC; ++k)
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) Vl[vidx(k, s)] = rv[k][s];
-    if (pc) wadd(pv, 4, 1.0);   // p^ = M^-1 p
     if (!matvec(pv, tv)) return -1;
     ++mv;
     int jc = col();
-    double rvv = 0.0, rm = 0.0, cs[KC];
+    double rvv = 0.0, rm = 0.0;
 #pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      cs[k] = 0.0;
+    for (int k = 0; k < KC; ++k)
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) {
         const double v = pv[k][s] - tv[k][s];
@@ -963,15 +580,12 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         if (own(jc, k, s)) {
           rvv += rh_at(jc, k, s) * v;
           rm = nan_max(rm, fabs(rv[k][s]));
-          cs[k] += v;
         }
       }
-    }
     part[0] = rvv;
     part[1] = rm;
-    if (pc) agg_sums(cs);
-    double xq[KC][SMAX];   // x of the own points, for x += alpha p^
-    if (!reduce(part, 2, 2u, pc, [&] {
+    double xq[KC][SMAX];   // x of the own points, for x += alpha p
+    if (!reduce(part, 2, 2u, [&] {
           const int jq = col();
 #pragma unroll
           for (int k = 0; k < KC; ++k)
@@ -979,17 +593,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
         }))
       return -1;
-    if (pc) coarse_y(1);
-#ifdef AIY_DIAG_PC
-    if (blockIdx.x == 0 && tid == 0 && mv < 400)
-      printf("[pc] it mv=%d <rh,v>=%.3e max|r|=%.3e Yv0=%.3e Zp0=%.3e\n", mv, s_res[0], s_res[1], s_Y[1][0], s_Y[4][0]);
-#endif
     if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
-      restart = true;
-      continue;
-    }
-    if (pc && !first && builds < r.pc_builds && s_res[1] < r.pc_drop * res_build) {
-      rebuild = true;   // coarse operator from the improved iterate
       restart = true;
       continue;
     }
@@ -1001,7 +605,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       mv_best = mv;
     } else if (mv - mv_best > kHkStall) {
       ++seed;
-      pc = false;   // a stalled preconditioned solve goes on plain
       best = __builtin_inf();
       restart = true;
       continue;
@@ -1012,7 +615,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       restart = true;
       continue;
     }
-    // x += alpha p^; p^ -> HBM scratch; s = r - alpha v (in rv); s^ = M^-1 s; t = s^ - T s^
+    // x += alpha p; p -> HBM scratch; s = r - alpha v (in rv); t = s - T s (in tv)
     jc = col();
 #pragma unroll
     for (int k = 0; k < KC; ++k)
@@ -1025,11 +628,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         }
         rv[k][s] -= alpha * Vl[vidx(k, s)];
       }
-    if (pc) {
-      if (tid < per) s_Y[6][tid] = s_Y[0][tid] - alpha * s_Y[1][tid];   // Ys = Yr - alpha Yv
-      __syncthreads();
-      wadd(rv, 6, 1.0);
-    }
     if (!matvec(rv, tv)) return -1;
     ++mv;
     jc = col();
@@ -1037,13 +635,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 #pragma unroll
     for (int k = 0; k < KC; ++k)
 #pragma unroll
-      for (int s = 0; s < SMAX; ++s) tv[k][s] = rv[k][s] - tv[k][s];   // t = s^ - T s^
-    if (pc) wadd(rv, 6, -1.0);   // s = s^ - W Ys
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      cs[k] = 0.0;
-#pragma unroll
       for (int s = 0; s < SMAX; ++s) {
+        tv[k][s] = rv[k][s] - tv[k][s];
         if (own(jc, k, s)) {
           const double h = rh_at(jc, k, s);
           ts += tv[k][s] * rv[k][s];
@@ -1051,18 +644,15 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           rs += h * rv[k][s];
           rt += h * tv[k][s];
           sm = nan_max(sm, fabs(rv[k][s]));
-          cs[k] += tv[k][s];
         }
       }
-    }
     part[0] = ts;
     part[1] = tt;
     part[2] = rs;
     part[3] = rt;
     part[4] = sm;
-    if (pc) agg_sums(cs);
-    double pq[KC][SMAX];   // x and p^ of the own points, for x += omega s and the new p
-    if (!reduce(part, 5, 16u, pc, [&] {
+    double pq[KC][SMAX];   // x and p of the own points, for x += omega s and the new p
+    if (!reduce(part, 5, 16u, [&] {
           const int jq = col();
 #pragma unroll
           for (int k = 0; k < KC; ++k)
@@ -1074,7 +664,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             }
         }))
       return -1;
-    if (pc) coarse_y(2);
     double omega = (s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1];
     if (!(fabs(omega) < 1e300)) omega = 0.0;
     if (omega == 0.0) {   // s already below tol (x + alpha p is the answer), or <t, t> = 0: verify
@@ -1084,8 +673,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     const double rho2 = s_res[2] - omega * s_res[3];
     const double beta = (rho2 / rho) * (alpha / omega);
     rho = rho2;
-    // x += omega s^ (fine part here, W Ys into Yx); r = s - omega t; p = r + beta (p - omega v)
-    // with p = p^ - W Yp: the stored vector r + beta (p^ - omega v) and Zp = Yp' - beta Yp
+    // x += omega s; r = s - omega t; p = r + beta (p - omega v)
     jc = col();
 #pragma unroll
     for (int k = 0; k < KC; ++k)
@@ -1097,17 +685,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         rv[k][s] = rv[k][s] - omega * tv[k][s];
         pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
       }
-    if (pc) {
-      if (tid < per) {
-        const int i = tid;
-        s_Y[5][i] += omega * s_Y[6][i];                                   // Yx
-        s_Y[0][i] = s_Y[6][i] - omega * s_Y[2][i];                        // Yr = Ys - omega Yt
-        const double yp = s_Y[0][i] + beta * (s_Y[3][i] - omega * s_Y[1][i]);
-        s_Y[4][i] = yp - beta * s_Y[3][i];                                // Zp
-        s_Y[3][i] = yp;                                                   // Yp
-      }
-      __syncthreads();
-    }
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }
 #ifdef AIY_DIAG_PHASES
@@ -1124,12 +701,23 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 // carries a lot of live state of its own (ge_resident.hip's search loop) would otherwise
 // force the solve's registers into scratch; the call costs a few register saves per
 // solve.  The span buffer / v share the caller's dynamic LDS.
-template <int SMAX, int KC, int TH, bool PC>
+template <int SMAX, int KC, int TH>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn[];
-  AIY_HK_SHARED(SMAX, KC, TH, hk_dyn);
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  const HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH, PC>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;

@@ -42,14 +42,25 @@ namespace aiy {
 template <int SMAX, int KC, int TH>
 __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   extern __shared__ double Tacc[];
-  AIY_HK_SHARED(SMAX, KC, TH, Tacc);
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];   // cf | cn << 8 (cf, cn <= kHcCand): LDS for 25 states
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  const HkShared<SMAX, KC, TH> L{Tacc, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop};
   const int G = r.G, S = r.S, n_a = r.n_a;
   const int lc = blockIdx.x / G;
   const int w = blockIdx.x - lc * G;
   const int cal = r.cal0 + lc;
   const size_t row0 = (size_t)cal * S;
   HkArgs a;
-  a.G = G; a.S = S; a.n_a = n_a; a.cap = r.cap; a.w = w; a.nj = r.nj;
+  a.G = G; a.S = S; a.n_a = n_a; a.cap = r.cap; a.w = w;
   a.j0 = w * r.nj;
   a.j1 = min(a.j0 + r.nj, n_a);
   a.LO = to_global(r.lo + row0 * n_a);
@@ -65,11 +76,6 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   a.tol = r.tolv ? r.tolv[cal] : r.tol;
   a.max_iter = r.max_iter;
   a.err = to_global(r.err);
-  a.pc_per = 0;   // plain BiCGSTAB (the preconditioned solve runs in the device-resident GE search)
-  a.pc_builds = 0;
-  a.pc_drop = 0.0;
-  a.Wg = a.Tc = a.Mc = a.Bi = to_global((double*)nullptr);
-  a.agran = to_global((unsigned long long*)nullptr);
   unsigned nb = 0, ne = 0;
   const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;

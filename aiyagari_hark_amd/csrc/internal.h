@@ -58,7 +58,6 @@ struct aiy_handle {
   // device-resident GE search (ge_resident.hip)
   bool ge_resident = false;          // AIY_OPT_GE_RESIDENT
   int cu_limit = 0;                  // AIY_OPT_CU_LIMIT: compute units resident launches may fill (0: all)
-  int hist_precond = 0;              // AIY_OPT_HIST_PRECOND: coarse builds per solve (0: plain BiCGSTAB)
   void* d_ge = nullptr;              // tables, masses, lottery, cluster sync of the launch
   size_t ge_cap = 0;
   hipEvent_t ge_ev[2] = {nullptr, nullptr};

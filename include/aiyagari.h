@@ -348,13 +348,6 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     and every cluster fits the device at once; else the host loop */
 #define AIY_OPT_CU_LIMIT 11       /* compute units the resident launches of this handle may fill
                                     (0: the device's; several processes sharing one GPU: a share) */
-#define AIY_OPT_HIST_PRECOND 12   /* device-resident GE search: BiCGSTAB right-preconditioned by a
-                                    two-level aggregation (coarse chain of contiguous asset
-                                    intervals, weights from the iterate, rebuilt as the residual
-                                    falls); value = coarse builds per distribution solve (default 0:
-                                    plain BiCGSTAB; experimental -- fewer matvecs on the slow cells,
-                                    but not robust where the coarse chain has several closed
-                                    classes).  The stopping rule is unchanged */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

@@ -72,27 +72,3 @@ def test_resident_default_sweep_and_stats(gpu):
     assert np.all(res.status == 0)
     ref = solve_table2(table2_calibrations(), n_a=2000, device=gpu, method="brent", resident=False)
     assert np.max(np.abs(res.r - ref.r)) <= 2e-7
-
-
-def test_preconditioned_distribution_solves(gpu):
-    """The two-level preconditioner of the resident BiCGSTAB solves (AIY_OPT_HIST_PRECOND)
-    keeps the stopping rule, so the roots agree with plain BiCGSTAB to the search tolerance,
-    in fewer matvecs."""
-    from aiyagari_hark_amd import _lib
-    from aiyagari_hark_amd.stationary import solve_table2
-    cals = _cells(6)
-    h = _lib.handle(gpu.index)
-    kw = dict(n_a=4000, device=gpu, method="brent", resident=True)
-    try:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_PRECOND, 0), "opt")
-        plain = solve_table2(cals, **kw)
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_PRECOND, 3), "opt")
-        pre = solve_table2(cals, **kw)
-    finally:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_PRECOND, 0), "opt")
-    mv_plain, mv_pre = int(np.sum(plain.hist_iters[0])), int(np.sum(pre.hist_iters[0]))
-    print(f"\nmatvecs plain {mv_plain} preconditioned {mv_pre}; r plain {plain.r} pre {pre.r}")
-    assert np.all(pre.status == 0)
-    assert np.max(np.abs(pre.r - plain.r)) <= 2e-7
-    assert np.max(np.abs(pre.KtoY - plain.KtoY) / plain.KtoY) <= 2e-6
-    assert mv_pre < mv_plain

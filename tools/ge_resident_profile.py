@@ -27,7 +27,6 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cells", type=int, default=24)
     ap.add_argument("--cluster-cap", type=int, default=0)
-    ap.add_argument("--precond", type=int, default=-1, help="AIY_OPT_HIST_PRECOND (coarse builds per solve; -1: default)")
     ap.add_argument("--modes", default="resident,host")
     args = ap.parse_args()
     from aiyagari_hark_amd import _lib
@@ -37,8 +36,6 @@ def main():
     h = _lib.handle(0)
     if args.cluster_cap:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, args.cluster_cap), "opt")
-    if args.precond >= 0:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_PRECOND, args.precond), "opt")
     out = {}
     for mode in args.modes.split(","):
         kw = dict(n_a=args.n_a, device=dev, method="brent", resident=mode == "resident")

@@ -25,12 +25,9 @@ for step in "$@"; do
   case $step in
     resident) run resident 300 $PYT -s tests/test_gpu_ge_resident.py ;;
     profile) run profile 300 python -u tools/ge_resident_profile.py ;;
-    pc0) run pc0 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --precond 0 ;;
-    pc3) run pc3 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --precond 3 ;;
     g12) run g12 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 12 ;;
     g6) run g6 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 6 ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
-    pc1) run pc1 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --precond 1 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
