@@ -37,6 +37,7 @@ AIY_OPT_HIST_ACCEL = 8
 AIY_OPT_HIST_KRYLOV = 9
 AIY_OPT_GE_RESIDENT = 10
 AIY_OPT_CU_LIMIT = 11
+AIY_OPT_GE_REBALANCE = 12
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

@@ -60,8 +60,9 @@ struct GeCalDev {
   double alpha, delta, disc, r_lo, r_hi;
 };
 
+struct GeState;
 struct GeRun {
-  int n_cal, S, n_a, G, nj, cap, n_work;
+  int n_cal, S, n_a, G, nj, cap, n_work;   // n_work = G x (calibrations of this launch)
   const double* a_grid;   // [n_cal][n_a]
   const double* P;        // [n_cal][S][S]
   const double* lab;      // [n_cal][S]
@@ -78,10 +79,19 @@ struct GeRun {
   double* pg;             // [n_cal][S][n_a] BiCGSTAB p rows
   int* lo;                // [n_cal][S][n_a]
   double* wlo;            // [n_cal][S][n_a]
-  double* slab;           // [n_cal][G][2][cap]
-  int* span;              // [n_cal][G][SMAX][4]
-  unsigned* ctr;          // [n_cal][kHcCtrStride]
-  unsigned long long* gran;   // [n_cal][2][G][kHcRedRec]
+  double* slab;           // [launch cals][G][2][cap]
+  int* span;              // [launch cals][G][SMAX][4]
+  unsigned* ctr;          // [launch cals][kHcCtrStride]
+  unsigned long long* gran;   // [launch cals][2][G][kHcRedRec]
+  // rebalancing: a launch covers some calibrations (cal_ids) and stops at the next evaluation
+  // boundary of every cluster once stop_at of them have finished; stopped ones save their
+  // search state and the host relaunches them with larger clusters
+  const int* cal_ids;     // [launch cals] cluster -> calibration
+  GeState* saved;         // [n_cal] search state of a stopped calibration
+  const int* resume;      // [n_cal] 1: start from saved[cal]
+  unsigned* done_ctr;     // calibrations of this launch whose search has ended
+  int stop_at;            // 0: never stop
+  int* out_done;          // [n_cal] 1: search ended (outputs written), 0: stopped
   unsigned* err;
   double* out_r;
   double* out_K;
@@ -413,7 +423,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
   const int u = (blockIdx.x & 7) * per + (blockIdx.x >> 3);   // XCD-contiguous work order
   if (u >= g.n_work) return;
   const int G = g.G, S = g.S, n_a = g.n_a, n1 = n_a + 1;
-  const int cal = u / G, w = u - cal * G;
+  const int lc = u / G, w = u - lc * G;   // launch-local cluster, workgroup in it
+  const int cal = g.cal_ids[lc];
   const int tid = threadIdx.x;
   const int j0 = w * g.nj, j1 = min(j0 + g.nj, n_a);
   const double* a_grid = g.a_grid + (size_t)cal * n_a;
@@ -428,9 +439,9 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
   double* PX = g.pmass + row0;
   int* LO = g.lo + row0;
   double* WL = g.wlo + row0;
-  unsigned* ctr = g.ctr + (size_t)cal * kHcCtrStride;
+  unsigned* ctr = g.ctr + (size_t)lc * kHcCtrStride;
   unsigned long long* cw = reinterpret_cast<unsigned long long*>(ctr + 2);   // counting-barrier words
-  unsigned long long* gran = g.gran + (size_t)cal * 2 * G * kHcRedRec;
+  unsigned long long* gran = g.gran + (size_t)lc * 2 * G * kHcRedRec;
   unsigned nb = 0, ne = 0;   // plain barriers / reductions passed (hk_solve counts on)
   const int pk = gam == 1.0 ? 1 : (gam == 3.0 ? 3 : (gam == 5.0 ? 5 : 0));
 
@@ -438,18 +449,23 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
   for (int q = tid; q < S * S; q += TH) s_Pe[q] = g.P[(size_t)cal * S * S + q];
   for (int q = tid; q < kGeMaxTiles * SMAX; q += TH) s_hint[q] = -1;
   if (tid == 0) {
-    st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method);
-    st.r_cur = st.r_prev = 0.0;
-    st.Ks = 0.0;
-    st.steps = 0;
-    st.refine = 0;
-    st.status = 0;
-    st.cyc_sum = st.its_sum = 0;
-    st.nc_prev[0] = st.nc_prev[1] = 0u;
+    if (g.resume[cal]) {   // a calibration stopped by an earlier launch: its search goes on
+      st = g.saved[cal];
+      st.t0 = __builtin_amdgcn_s_memrealtime() - st.t0;   // saved: the time spent so far
+    } else {
+      st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method);
+      st.r_cur = st.r_prev = 0.0;
+      st.Ks = 0.0;
+      st.steps = 0;
+      st.refine = 0;
+      st.status = 0;
+      st.cyc_sum = st.its_sum = 0;
+      for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
+      st.t_egm = st.t_lot = st.t_hist = st.t_k = 0ull;
+      st.t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    st.nc_prev[0] = st.nc_prev[1] = 0u;   // this launch's counting-barrier words start at 0
     st.nbc = 0u;
-    for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
-    st.t_egm = st.t_lot = st.t_hist = st.t_k = 0ull;
-    st.t0 = __builtin_amdgcn_s_memrealtime();
   }
   __syncthreads();
   auto plain_barrier = [&]() -> bool {
@@ -458,7 +474,33 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     return hc_barrier(g.err, ctr, (unsigned)G * nb, &s_flag);
   };
 
+  bool stopped = false;
   while (!st.rs.done && st.steps < g.max_steps) {
+    // ---- rebalancing stop: once stop_at calibrations of the launch have finished, the
+    //      cluster leaves at this evaluation boundary (the decision: any workgroup saw it,
+    //      counted on the cluster's barrier, so every workgroup takes it) ----
+    if (g.stop_at > 0 && st.steps > 0) {
+      unsigned flag = 0u;
+      if (tid == 0) {
+        flag = __hip_atomic_load(to_global(g.done_ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                       (unsigned)g.stop_at ? 1u : 0u;
+        ++st.nbc;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const unsigned k = st.nbc, par = k & 1u;
+      if (!hc_barrier_count(g.err, &cw[par], (unsigned)G * ((k + par) / 2), flag, &s_nc, &s_flag)) return;
+      if (tid == 0) {
+        const unsigned dlt = s_nc - st.nc_prev[par];
+        st.nc_prev[par] = s_nc;
+        st.stop = dlt != 0u;
+      }
+      __syncthreads();
+      if (st.stop) {
+        stopped = true;
+        break;
+      }
+    }
     // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
     if (tid == 0) {
       const double r = st.rs.x, a = cd.alpha, d = cd.delta;
@@ -670,8 +712,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
       hk.LO = to_global((const int*)LO); hk.WL = to_global((const double*)WL); hk.X = to_global(X);
       hk.Pg = to_global(g.pg + row0); hk.Vg = to_global((double*)nullptr);
-      hk.slab_cl = to_global(g.slab + (size_t)cal * G * 2 * g.cap);
-      hk.span_cl = to_global(g.span + (size_t)cal * G * SMAX * 4);
+      hk.slab_cl = to_global(g.slab + (size_t)lc * G * 2 * g.cap);
+      hk.span_cl = to_global(g.span + (size_t)lc * G * SMAX * 4);
       hk.ctr = to_global(ctr); hk.gran = to_global(gran); hk.Pc = to_global(g.P + (size_t)cal * S * S);
       hk.max_iter = g.max_hist; hk.err = to_global(g.err);
       hk.tol = st.htol;
@@ -709,7 +751,17 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     }
     __syncthreads();
   }
+  if (stopped) {
+    if (w == 0 && tid == 0) {
+      st.t0 = __builtin_amdgcn_s_memrealtime() - st.t0;
+      g.saved[cal] = st;
+      g.out_done[cal] = 0;
+    }
+    return;
+  }
   if (w == 0 && tid == 0) {
+    __hip_atomic_fetch_add(to_global(g.done_ctr), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g.out_done[cal] = 1;
     const double r = st.rs.x, a = cd.alpha, d = cd.delta;
     g.out_r[cal] = r;
     g.out_K[cal] = pow(a / (r + d), 1.0 / (1.0 - a));
@@ -784,9 +836,13 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, err, cal, outd, outi, prof, run, bytes;
+  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
+      bytes;
 };
-static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
+// Per-calibration arrays (kept across the rebalancing launches) first, then the per-launch
+// cluster arrays sized for the most workgroups any launch can hold (cus) and the largest span
+// capacity (cap_max doubles).
+static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_max) {
   GeScratch L;
   size_t o = 0;
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
@@ -794,39 +850,41 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int G, int cap) {
   L.tab = take((size_t)n_cal * kGeBufs * 2 * S * (n_a + 1) * sizeof(double));
   L.mass = take(pts * 8); L.pmass = take(pts * 8); L.pg = take(pts * 8);
   L.lo = take(pts * 4); L.wlo = take(pts * 8);
-  L.slab = take((size_t)n_cal * G * 2 * cap * sizeof(double));
-  L.span = take((size_t)n_cal * G * 8 * 4 * sizeof(int));
+  L.slab = take((size_t)cus * 2 * cap_max * sizeof(double));
+  L.span = take((size_t)cus * 8 * 4 * sizeof(int));
   L.ctr = take((size_t)n_cal * kHcCtrStride * sizeof(unsigned));
-  L.gran = take((size_t)n_cal * 2 * G * kHcRedRec * sizeof(unsigned long long));
+  L.gran = take((size_t)cus * 2 * kHcRedRec * sizeof(unsigned long long));
+  L.ids = take((size_t)n_cal * sizeof(int));
+  L.saved = take((size_t)n_cal * sizeof(GeState));
+  L.resume = take((size_t)n_cal * sizeof(int));
+  L.done = take((size_t)n_cal * sizeof(int));
   L.err = take(256);
   L.cal = take((size_t)n_cal * sizeof(GeCalDev));
   L.outd = take((size_t)n_cal * 3 * sizeof(double));
   L.outi = take((size_t)n_cal * 4 * sizeof(int));
   L.prof = take((size_t)n_cal * kGeProf * sizeof(double));
-  L.run = take(sizeof(GeRun));
   L.bytes = o;
   return L;
 }
 
-// The whole search in one launch when the shape allows it (1: done; 0: not applicable, the
-// caller runs the host-driven loop; < 0: error).
+// The whole search on device when the shape allows it (1: done; 0: not applicable, the caller
+// runs the host-driven loop; < 0: error).  With rebalancing (AIY_OPT_GE_REBALANCE = q > 0,
+// default 50) a launch whose calibrations are more than 4 stops every cluster at its next
+// evaluation boundary once q % of them have finished, and the unfinished ones are launched
+// again with the freed compute units (a cluster's time scales with its columns per CU): with
+// q = 50 the 24 Table II cells run as 24 x 10, then ~12 x 21, ~6 x 32, ~3 x 32 workgroups.
 int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, const aiy_ge_options* o, double* r_out,
                                double* K_out, double* Ks_out, int32_t* steps_out, int32_t* cyc_out,
                                int32_t* its_out, int32_t* status_out, hipStream_t st) {
   if (!h->ge_resident || o->accel >= 0) return 0;   // BiCGSTAB distribution solves only
   const int n_cal = M->n_cal, S = M->S, n_a = M->n_a;
-  GePlan p;
-  if (!ge_make_plan(h, n_cal, S, n_a, p)) return 0;
-  if (hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds) != hipSuccess || per_cu < 1) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, p.G, p.cap);
+  GePlan p0;
+  if (!ge_make_plan(h, n_cal, S, n_a, p0)) return 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) return 0;
+  if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
+  const int cap_max = (int)(kHcLdsTotal / sizeof(double));
+  const GeScratch L = ge_scratch_layout(n_cal, S, n_a, cus, cap_max);
   if (L.bytes > h->ge_cap) {
     if (h->d_ge) (void)hipFree(h->d_ge);
     h->d_ge = nullptr;
@@ -844,7 +902,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
     cals[c].r_hi = o->r_hi ? o->r_hi[c] : 1.0 / M->disc[c] - 1.0 - 1e-9;
   }
   GeRun g;
-  g.n_cal = n_cal; g.S = S; g.n_a = n_a; g.G = p.G; g.nj = p.nj; g.cap = p.cap; g.n_work = n_cal * p.G;
+  g.n_cal = n_cal; g.S = S; g.n_a = n_a;
   g.a_grid = M->a_grid; g.P = M->P; g.lab = M->lab; g.beta = M->beta; g.crra = M->crra;
   g.cal = reinterpret_cast<const GeCalDev*>(base + L.cal);
   g.method = o->method; g.r_tol = o->r_tol; g.egm_tol = o->egm_tol; g.hist_tol = o->hist_tol;
@@ -863,39 +921,87 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.span = reinterpret_cast<int*>(base + L.span);
   g.ctr = reinterpret_cast<unsigned*>(base + L.ctr);
   g.gran = reinterpret_cast<unsigned long long*>(base + L.gran);
+  int* d_ids = reinterpret_cast<int*>(base + L.ids);
+  int* d_resume = reinterpret_cast<int*>(base + L.resume);
+  g.cal_ids = d_ids;
+  g.saved = reinterpret_cast<GeState*>(base + L.saved);
+  g.resume = d_resume;
+  g.out_done = reinterpret_cast<int*>(base + L.done);
   g.err = reinterpret_cast<unsigned*>(base + L.err);
+  g.done_ctr = g.err + 1;
   double* outd = reinterpret_cast<double*>(base + L.outd);
   int* outi = reinterpret_cast<int*>(base + L.outi);
   g.out_r = outd; g.out_K = outd + n_cal; g.out_Ks = outd + 2 * n_cal;
   g.out_steps = outi; g.out_cyc = outi + n_cal; g.out_its = outi + 2 * n_cal; g.out_status = outi + 3 * n_cal;
   g.out_prof = reinterpret_cast<double*>(base + L.prof);
   AIY_HIP(h, hipMemcpyAsync(base + L.cal, cals.data(), sizeof(GeCalDev) * n_cal, hipMemcpyHostToDevice, st));
-  AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n_cal * kHcCtrStride * sizeof(unsigned), st));
-  AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n_cal * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
-  AIY_HIP(h, hipMemsetAsync(g.err, 0, 256, st));
+  AIY_HIP(h, hipMemsetAsync(d_resume, 0, (size_t)n_cal * sizeof(int), st));
+  AIY_HIP(h, hipMemsetAsync(g.out_done, 0, (size_t)n_cal * sizeof(int), st));
   for (hipEvent_t& e : h->ge_ev)
     if (!e) AIY_HIP(h, hipEventCreate(&e));
-  void* args[] = {&g};
-  AIY_HIP(h, hipEventRecord(h->ge_ev[0], st));
-  AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(p.th), args, p.lds, st));
-  AIY_HIP(h, hipEventRecord(h->ge_ev[1], st));
+  std::vector<int> active(n_cal), done(n_cal, 0), resume(n_cal, 0);
+  for (int c = 0; c < n_cal; ++c) active[c] = c;
+  h->ge_rounds = 0;
+  while (!active.empty()) {
+    const int n = (int)active.size();
+    GePlan p;
+    if (!ge_make_plan(h, n, S, n_a, p)) return fail(h, AIY_ERR_STATE, "device-resident GE: no plan for %d calibrations", n);
+    if (hipFuncSetAttribute(p.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
+      (void)hipGetLastError();
+      if (h->ge_rounds == 0) return 0;
+      return fail(h, AIY_ERR_STATE, "device-resident GE: dynamic LDS attribute");
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p.fn, p.th, p.lds) != hipSuccess || per_cu < 1) {
+      (void)hipGetLastError();
+      if (h->ge_rounds == 0) return 0;
+      return fail(h, AIY_ERR_STATE, "device-resident GE: occupancy query");
+    }
+    g.G = p.G; g.nj = p.nj; g.cap = p.cap; g.n_work = n * p.G;
+    g.stop_at = (h->ge_rebalance > 0 && n > 4) ? std::max(1, (n * h->ge_rebalance + 99) / 100) : 0;
+    std::vector<int> res_h(n_cal);
+    for (int c = 0; c < n_cal; ++c) res_h[c] = resume[c];
+    AIY_HIP(h, hipMemcpyAsync(d_ids, active.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+    AIY_HIP(h, hipMemcpyAsync(d_resume, res_h.data(), sizeof(int) * n_cal, hipMemcpyHostToDevice, st));
+    AIY_HIP(h, hipMemsetAsync(g.ctr, 0, (size_t)n * kHcCtrStride * sizeof(unsigned), st));
+    AIY_HIP(h, hipMemsetAsync(g.gran, 0, (size_t)n * 2 * p.G * kHcRedRec * sizeof(unsigned long long), st));
+    AIY_HIP(h, hipMemsetAsync(g.err, 0, 256, st));
+    void* args[] = {&g};
+    AIY_HIP(h, hipEventRecord(h->ge_ev[0], st));
+    AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(p.th), args, p.lds, st));
+    AIY_HIP(h, hipEventRecord(h->ge_ev[1], st));
+    unsigned err = 0;
+    AIY_HIP(h, hipMemcpyAsync(&err, g.err, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipMemcpyAsync(done.data(), g.out_done, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
+    AIY_HIP(h, hipStreamSynchronize(st));
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ge_ev[0], h->ge_ev[1]) == hipSuccess) {
+      h->ge_ms_sum += ms;
+      h->ge_launches += 1;
+    }
+    ++h->ge_rounds;
+    if (err == 1u)
+      return fail(h, AIY_ERR_STATE, "device-resident GE: cluster barrier timed out (workgroups not co-resident?)");
+    if (err) return fail(h, AIY_ERR_STATE, "device-resident GE: histogram shape does not fit (error %u)", err);
+    std::vector<int> next;
+    for (int c : active) {
+      if (!done[c]) {
+        next.push_back(c);
+        resume[c] = 1;
+      }
+    }
+    if ((int)next.size() == n && g.stop_at > 0)
+      return fail(h, AIY_ERR_STATE, "device-resident GE: a rebalancing launch finished no calibration");
+    active.swap(next);
+  }
   std::vector<double> hd(3 * (size_t)n_cal);
   std::vector<int> hi(4 * (size_t)n_cal);
-  unsigned err = 0;
-  AIY_HIP(h, hipMemcpyAsync(&err, g.err, sizeof(unsigned), hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(hd.data(), outd, sizeof(double) * 3 * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(hi.data(), outi, sizeof(int) * 4 * n_cal, hipMemcpyDeviceToHost, st));
   h->ge_prof.assign((size_t)n_cal * kGeProf, 0.0);
   AIY_HIP(h, hipMemcpyAsync(h->ge_prof.data(), g.out_prof, sizeof(double) * kGeProf * n_cal, hipMemcpyDeviceToHost,
                             st));
   AIY_HIP(h, hipStreamSynchronize(st));
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, h->ge_ev[0], h->ge_ev[1]) == hipSuccess) {
-    h->ge_ms_sum += ms;
-    h->ge_launches += 1;
-  }
-  if (err == 1u) return fail(h, AIY_ERR_STATE, "device-resident GE: cluster barrier timed out (workgroups not co-resident?)");
-  if (err) return fail(h, AIY_ERR_STATE, "device-resident GE: histogram shape does not fit (error %u)", err);
   long long cyc = 0, its = 0;
   int steps = 0;
   for (int c = 0; c < n_cal; ++c) {

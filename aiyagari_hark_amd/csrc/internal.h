@@ -58,6 +58,8 @@ struct aiy_handle {
   // device-resident GE search (ge_resident.hip)
   bool ge_resident = false;          // AIY_OPT_GE_RESIDENT
   int cu_limit = 0;                  // AIY_OPT_CU_LIMIT: compute units resident launches may fill (0: all)
+  int ge_rebalance = 50;             // AIY_OPT_GE_REBALANCE: % finished that stops a launch (0: one launch)
+  int ge_rounds = 0;                 // launches of the last device-resident search
   void* d_ge = nullptr;              // tables, masses, lottery, cluster sync of the launch
   size_t ge_cap = 0;
   hipEvent_t ge_ev[2] = {nullptr, nullptr};

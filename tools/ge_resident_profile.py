@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--cells", type=int, default=24)
     ap.add_argument("--cluster-cap", type=int, default=0)
     ap.add_argument("--modes", default="resident,host")
+    ap.add_argument("--rebalance", type=int, default=-1, help="AIY_OPT_GE_REBALANCE (-1: default)")
     args = ap.parse_args()
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
@@ -36,6 +37,8 @@ def main():
     h = _lib.handle(0)
     if args.cluster_cap:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, args.cluster_cap), "opt")
+    if args.rebalance >= 0:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, args.rebalance), "opt")
     out = {}
     for mode in args.modes.split(","):
         kw = dict(n_a=args.n_a, device=dev, method="brent", resident=mode == "resident")

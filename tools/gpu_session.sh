@@ -27,6 +27,11 @@ for step in "$@"; do
     profile) run profile 300 python -u tools/ge_resident_profile.py ;;
     g12) run g12 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 12 ;;
     g6) run g6 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 6 ;;
+    q25) run q25 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 25 ;;
+    q34) run q34 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 34 ;;
+    q67) run q67 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 67 ;;
+    q80) run q80 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 80 ;;
+    g24off) run g24off 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 0 ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
