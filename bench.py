@@ -719,14 +719,17 @@ def main():
         "roofline": {"kernel": t2["kernel"], "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("hist_bicg_kernel",
-                                            scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV),
+                     "traffic": (pmc_traffic("ge_cluster_kernel") if t2["resident"] else
+                                 pmc_traffic("hist_bicg_kernel",
+                                             scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV)),
                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
                      "avg_launch_ms": t2["hist_avg_launch_ms"],
-                     "launch": ("one whole sweep of the rank's calibrations (every K_s(r) evaluation of every "
-                                "root search): 52 B per state x node point per matvec of the distribution solves "
-                                "(28 B lottery push + mix, 24 B iterate updates) + 32 B per state x node per EGM "
-                                "cycle" if t2["resident"] else
+                     "launch": ("one launch of the device-resident search (a sweep of the rank's calibrations "
+                                "runs as a few rebalancing launches, every K_s(r) evaluation of every root search "
+                                "in one of them): 52 B per state x node point per matvec of the distribution "
+                                "solves (28 B lottery push + mix, 24 B iterate updates) + 32 B per state x node "
+                                "per EGM cycle; traffic: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of the "
+                                "same sweep" if t2["resident"] else
                                 "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
                                 "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
                                 "updates)"),
