@@ -2,8 +2,9 @@
 full-size fixtures made by the CPU oracle (tests/golden/make_golden_fullsize.py,
 tests/golden/make_golden_c3.py):
 
-* configs[2] -- the bench's own Table II sweep (solve_table2(method="brent"): 3 independent
-  groups, secant starts, loose bracketing, EGM extrapolation, BiCGSTAB distribution) at
+* configs[2] -- the bench's own Table II sweep (solve_table2(method="brent"): the
+  device-resident search with rebalancing relaunches, secant starts, loose bracketing, EGM
+  extrapolation, BiCGSTAB distribution) at
   N_a = 10 000 against the oracle's ge_bisect of all 24 cells (cold EGM to 1e-8, cold Young
   histogram to 1e-12, bisection to 1e-7): r within R_TOL, K/Y within KY_RTOL relative;
 * configs[4] -- the 3 stress cells (25-state Rouwenhorst, N_a = 50 000) the same way, and

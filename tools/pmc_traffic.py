@@ -48,13 +48,21 @@ def point_iters(log_path):
 def main():
     fd, wd, out = sys.argv[1:4]
     pts = point_iters(sys.argv[4]) if len(sys.argv) > 4 else 0
-    fetch = per_kernel(fd, "FETCH_SIZE")
-    write = per_kernel(wd, "WRITE_SIZE")
+    def by_short(d):   # template instantiations of one kernel pooled (mean over all their dispatches)
+        agg = collections.defaultdict(lambda: [0.0, 0, []])
+        for k, (mean, n) in d.items():
+            short = k.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+            agg[short][0] += mean * n
+            agg[short][1] += n
+            agg[short][2].append(k)
+        return {s: (t / max(1, n), n, names) for s, (t, n, names) in agg.items()}
+    fetch = by_short(per_kernel(fd, "FETCH_SIZE"))
+    write = by_short(per_kernel(wd, "WRITE_SIZE"))
     res = {}
-    for k in set(fetch) | set(write):
-        f_kb, nf = fetch.get(k, (0.0, 0))
-        w_kb, nw = write.get(k, (0.0, 0))
-        short = k.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+    for short in set(fetch) | set(write):
+        f_kb, nf, names_f = fetch.get(short, (0.0, 0, []))
+        w_kb, nw, names_w = write.get(short, (0.0, 0, []))
+        k = " | ".join(sorted(set(names_f) | set(names_w)))
         res[short] = dict(kernel=k, fetch_kb_raw=f_kb, write_kb=w_kb, dispatches=[nf, nw],
                           hbm_bytes_per_launch=(2.0 * f_kb + w_kb) * 1024.0,
                           correction="FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1")
