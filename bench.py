@@ -552,6 +552,19 @@ def table2_reference_leg(world, rank, dev, agents=350):
                         "one EconomyBatch per rank"}
 
 
+def pmc_traffic_per_sweep(kernel, launches_per_sweep):
+    """HBM bytes per launch of a kernel whose committed PMC passes each profiled ONE sweep
+    (hbm_bytes_total: FETCH x2 + WRITE summed over the sweep's dispatches; the number of
+    rebalancing launches can differ between the two passes), spread over this run's
+    launches per sweep; or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))[kernel]
+        return float(d["hbm_bytes_total"]) / max(1e-9, float(launches_per_sweep))
+    except Exception:
+        return None
+
+
 def pmc_traffic(kernel, scale=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
@@ -719,7 +732,8 @@ def main():
         "roofline": {"kernel": t2["kernel"], "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
-                     "traffic": (pmc_traffic("ge_cluster_kernel") if t2["resident"] else
+                     "traffic": (pmc_traffic_per_sweep("ge_cluster_kernel", t2["hist_launches_per_sweep"])
+                                 if t2["resident"] else
                                  pmc_traffic("hist_bicg_kernel",
                                              scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV)),
                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],

@@ -47,7 +47,7 @@ def point_iters(log_path):
 
 def main():
     fd, wd, out = sys.argv[1:4]
-    pts = point_iters(sys.argv[4]) if len(sys.argv) > 4 else 0
+    pts = point_iters(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else 0
     def by_short(d):   # template instantiations of one kernel pooled (mean over all their dispatches)
         agg = collections.defaultdict(lambda: [0.0, 0, []])
         for k, (mean, n) in d.items():
@@ -65,6 +65,7 @@ def main():
         k = " | ".join(sorted(set(names_f) | set(names_w)))
         res[short] = dict(kernel=k, fetch_kb_raw=f_kb, write_kb=w_kb, dispatches=[nf, nw],
                           hbm_bytes_per_launch=(2.0 * f_kb + w_kb) * 1024.0,
+                          hbm_bytes_total=(2.0 * f_kb * nf + w_kb * nw) * 1024.0,
                           correction="FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1")
         if short in ("hist_cluster_kernel", "hist_bicg_kernel") and pts > 0:
             res[short]["point_iters"] = pts
