@@ -457,7 +457,7 @@ def configs3_leg(args, world, rank, dev):
                us_per_period=1e6 * el / T, K_final=float(K_hist[T - 1]), K_first=[float(x) for x in K_hist[:5]],
                roofline={"kernel": kern, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("sim_resident_kernel_stream") if world == 1 else None,
+                         "traffic": pmc_traffic_periods("sim_resident_kernel_stream", T) if world == 1 else None,
                          "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": kern_ms},
                workload=f"BASELINE configs[3]: {n_total} agents x {T} periods, agents sharded over {world} rank(s), "
                         "Philox by global agent index, per-period all-reduce of the asset sum when sharded "
@@ -561,6 +561,16 @@ def pmc_traffic_per_sweep(kernel, launches_per_sweep):
     try:
         d = json.load(open(path))[kernel]
         return float(d["hbm_bytes_total"]) / max(1e-9, float(launches_per_sweep))
+    except Exception:
+        return None
+
+
+def pmc_traffic_periods(kernel, periods):
+    """HBM bytes of a launch of `periods` panel periods from the committed PMC passes
+    (hbm_bytes_per_period), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[kernel]
+        return float(d["hbm_bytes_per_period"]) * periods
     except Exception:
         return None
 
