@@ -111,6 +111,7 @@ struct GeState {
   RootSearch rs;
   double R, wage, Kd, etol, htol, theta, r_cur, r_prev, Ks, dist, lam_prev, fext;
   int steps, loose, refine, warm_egm, secant, fresh_mass, status, n, stop, nan_stop, moved, extrap;
+  int in_hist;             // stopped (rebalancing) inside this evaluation's distribution solve
   int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
   long long cyc_sum, its_sum;
   unsigned long long t_egm, t_lot, t_hist, t_k, t0;
@@ -458,6 +459,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st.Ks = 0.0;
       st.steps = 0;
       st.refine = 0;
+      st.in_hist = 0;
       st.status = 0;
       st.cyc_sum = st.its_sum = 0;
       for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     // ---- rebalancing stop: once stop_at calibrations of the launch have finished, the
     //      cluster leaves at this evaluation boundary (the decision: any workgroup saw it,
     //      counted on the cluster's barrier, so every workgroup takes it) ----
-    if (g.stop_at > 0 && st.steps > 0) {
+    if (g.stop_at > 0 && st.steps > 0 && !st.in_hist) {
       unsigned flag = 0u;
       if (tid == 0) {
         flag = __hip_atomic_load(to_global(g.done_ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
@@ -501,209 +503,214 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
         break;
       }
     }
-    // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
-    if (tid == 0) {
-      const double r = st.rs.x, a = cd.alpha, d = cd.delta;
-      const double KtoL = pow(a / (r + d), 1.0 / (1.0 - a));
-      st.R = 1.0 + r;
-      st.wage = (1.0 - a) * pow(KtoL, a);
-      st.Kd = KtoL;
-      st.loose = g.loose && g.method == 1 && !st.rs.brent && !st.rs.done && !st.refine;
-      st.etol = st.loose ? fmax(g.egm_tol, AIY_GE_LOOSE_EGM) : g.egm_tol;
-      st.htol = st.loose ? fmax(g.hist_tol, AIY_GE_LOOSE_HIST) : g.hist_tol;
-      st.warm_egm = g.warm_egm && st.steps > 0;
-      st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
-      st.fresh_mass = !(g.warm_hist && st.steps > 0);
-      double th = 0.0;
-      if (st.secant) {
-        const double den = st.r_cur - st.r_prev;
-        th = den != 0.0 ? (r - st.r_cur) / den : 0.0;
-        th = isfinite(th) ? fmax(-1.0, fmin(1.0, th)) : 0.0;
-      }
-      st.theta = th;
-      st.extrap = g.extrap;
-      st.moved = 0;
-    }
-    __syncthreads();
-    if (tid < S) s_Wl[tid] = st.wage * g.lab[(size_t)cal * S + tid];   // W l(s') (mNextArray, AS:1024)
-    const double R = st.R, theta = st.theta;
-    // ---- starting tables: the secant start into `init` (own nodes), else cur ----
-    const bool secant = st.secant != 0, warm = st.warm_egm != 0;
-    const int b_cur = st.buf[2], b_prev = st.buf[3], b_init = st.buf[4];
-    if (secant) {
-      for (int s = 0; s < S; ++s) {
-        for (int k = j0 + tid; k < j1; k += TH) {
-          const size_t o = (size_t)s * n1 + k + 1;
-          const double cm = load_f64_agent(&tabm(b_cur)[o]), pm = load_f64_agent(&tabm(b_prev)[o]);
-          const double cc = load_f64_agent(&tabc(b_cur)[o]), pc = load_f64_agent(&tabc(b_prev)[o]);
-          store_f64_agent(&tabm(b_init)[o], theta == 0.0 ? cm : cm + theta * (cm - pm));
-          store_f64_agent(&tabc(b_init)[o], theta == 0.0 ? cc : cc + theta * (cc - pc));
-        }
-        if (j0 == 0 && tid == 0) {
-          store_f64_agent(&tabm(b_init)[(size_t)s * n1], kBorrowNode);
-          store_f64_agent(&tabc(b_init)[(size_t)s * n1], kBorrowNode);
-        }
-      }
-    }
-    // ---- the household solve ([HARK] solve_agent: cycles until the sup-norm change of the
-    //      tables is <= tol, NaN stops; cold: cycle 1 from the terminal guess) ----
+    // a calibration stopped inside its distribution solve resumes there (prices, tables,
+    // lottery and the iterate are in the saved state and HBM)
     unsigned long long tp = __builtin_amdgcn_s_memrealtime();
-    const double* init_m = secant ? tabm(b_init) : (warm ? tabm(b_cur) : nullptr);
-    const double* init_c = secant ? tabc(b_init) : (warm ? tabc(b_cur) : nullptr);
-    int final_buf = -1;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-      if (!plain_barrier()) return;   // every workgroup's start tables visible
-      const bool ext = st.extrap != 0 && attempt == 0;
+    if (!st.in_hist) {
+      // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
       if (tid == 0) {
-        st.lam_prev = -1.0;
+        const double r = st.rs.x, a = cd.alpha, d = cd.delta;
+        const double KtoL = pow(a / (r + d), 1.0 / (1.0 - a));
+        st.R = 1.0 + r;
+        st.wage = (1.0 - a) * pow(KtoL, a);
+        st.Kd = KtoL;
+        st.loose = g.loose && g.method == 1 && !st.rs.brent && !st.rs.done && !st.refine;
+        st.etol = st.loose ? fmax(g.egm_tol, AIY_GE_LOOSE_EGM) : g.egm_tol;
+        st.htol = st.loose ? fmax(g.hist_tol, AIY_GE_LOOSE_HIST) : g.hist_tol;
+        st.warm_egm = g.warm_egm && st.steps > 0;
+        st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
+        st.fresh_mass = !(g.warm_hist && st.steps > 0);
+        double th = 0.0;
+        if (st.secant) {
+          const double den = st.r_cur - st.r_prev;
+          th = den != 0.0 ? (r - st.r_cur) / den : 0.0;
+          th = isfinite(th) ? fmax(-1.0, fmin(1.0, th)) : 0.0;
+        }
+        st.theta = th;
+        st.extrap = g.extrap;
         st.moved = 0;
-        st.nan_stop = 0;
       }
-      int n = 1;
-      const int last_allowed = g.max_cyc + 1;
-      bool converged = false;
-      while (true) {
-        const int b_dst = st.buf[n & 1], b_src = st.buf[(n - 1) & 1];
-        const double* sm = n == 1 ? init_m : tabm(b_src);
-        const double* sc = n == 1 ? init_c : tabc(b_src);
-        const bool track = n >= 2;
-        double dl;
-        if (pk == 1)
-          dl = ge_egm_cycle_fn<SMAX, SC, 1, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                            gam);
-        else if (pk == 3)
-          dl = ge_egm_cycle_fn<SMAX, SC, 3, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                            gam);
-        else if (pk == 5)
-          dl = ge_egm_cycle_fn<SMAX, SC, 5, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                            gam);
-        else
-          dl = ge_egm_cycle_fn<SMAX, SC, 0, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                            gam);
-        // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
-        // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
-        const bool want_value = ext && n >= kGeExtrap - 1 &&
-                                ((n % kGeExtrap) == kGeExtrap - 1 || (n % kGeExtrap) == 0);
-        double dclu = 0.0;
-        bool go;
-        if (want_value) {
-          double v[1] = {dl};
-          if (!ge_reduce<TH>(gran, G, w, ne, v, 1, 1u, s_part, s_res, &s_flag, g.err)) return;
-          dclu = s_res[0];
-          go = dclu > st.etol;   // NaN: stop (HARK: go = distance > tolerance)
-          if (tid == 0) st.nan_stop = dclu != dclu;
-        } else {
-          const double dw = wave_nan_max(dl);
-          if ((tid & (kWave - 1)) == 0) s_part[0][tid / kWave] = dw;
-          __syncthreads();
-          unsigned flag = 0u;
-          if (tid == 0) {
-            double d = s_part[0][0];
-            for (int q = 1; q < TH / kWave; ++q) d = nan_max(d, s_part[0][q]);
-            flag = (d > st.etol ? 1u : 0u) | (d != d ? (1u << 16) : 0u);
-            ++st.nbc;
+      __syncthreads();
+      if (tid < S) s_Wl[tid] = st.wage * g.lab[(size_t)cal * S + tid];   // W l(s') (mNextArray, AS:1024)
+      const double R = st.R, theta = st.theta;
+      // ---- starting tables: the secant start into `init` (own nodes), else cur ----
+      const bool secant = st.secant != 0, warm = st.warm_egm != 0;
+      const int b_cur = st.buf[2], b_prev = st.buf[3], b_init = st.buf[4];
+      if (secant) {
+        for (int s = 0; s < S; ++s) {
+          for (int k = j0 + tid; k < j1; k += TH) {
+            const size_t o = (size_t)s * n1 + k + 1;
+            const double cm = load_f64_agent(&tabm(b_cur)[o]), pm = load_f64_agent(&tabm(b_prev)[o]);
+            const double cc = load_f64_agent(&tabc(b_cur)[o]), pc = load_f64_agent(&tabc(b_prev)[o]);
+            store_f64_agent(&tabm(b_init)[o], theta == 0.0 ? cm : cm + theta * (cm - pm));
+            store_f64_agent(&tabc(b_init)[o], theta == 0.0 ? cc : cc + theta * (cc - pc));
           }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          const unsigned k = st.nbc, par = k & 1u;
-          if (!hc_barrier_count(g.err, &cw[par], (unsigned)G * ((k + par) / 2), flag, &s_nc, &s_flag)) return;
-          if (tid == 0) {
-            const unsigned dlt = s_nc - st.nc_prev[par];
-            st.nc_prev[par] = s_nc;
-            st.stop = (dlt & 0xffffu) == 0u || (dlt >> 16) != 0u;
-            st.nan_stop = (dlt >> 16) != 0u;
+          if (j0 == 0 && tid == 0) {
+            store_f64_agent(&tabm(b_init)[(size_t)s * n1], kBorrowNode);
+            store_f64_agent(&tabc(b_init)[(size_t)s * n1], kBorrowNode);
           }
-          __syncthreads();
-          go = !st.stop;
         }
-        if (track && !go) {
-          converged = true;
-          break;
+      }
+      // ---- the household solve ([HARK] solve_agent: cycles until the sup-norm change of the
+      //      tables is <= tol, NaN stops; cold: cycle 1 from the terminal guess) ----
+      tp = __builtin_amdgcn_s_memrealtime();
+      const double* init_m = secant ? tabm(b_init) : (warm ? tabm(b_cur) : nullptr);
+      const double* init_c = secant ? tabc(b_init) : (warm ? tabc(b_cur) : nullptr);
+      int final_buf = -1;
+      for (int attempt = 0; attempt < 2; ++attempt) {
+        if (!plain_barrier()) return;   // every workgroup's start tables visible
+        const bool ext = st.extrap != 0 && attempt == 0;
+        if (tid == 0) {
+          st.lam_prev = -1.0;
+          st.moved = 0;
+          st.nan_stop = 0;
         }
-        if (n >= last_allowed) break;
-        // geometric extrapolation at the checks (ge.hip / egm.hip egm_extrap_kernel)
-        if (want_value && (n % kGeExtrap) == 0) {
-          if (tid == 0) {
-            const double d1 = dclu, d0 = st.dist, lam = d1 / d0;
-            st.fext = 0.0;
-            if (n >= 4 && d1 > 100.0 * st.etol && lam > 0.5 && lam < 0.999 && st.lam_prev > 0.0 &&
-                fabs(lam - st.lam_prev) < 0.2 * (1.0 - lam)) {
-              st.fext = lam / (1.0 - lam);
-              st.moved = 1;
+        int n = 1;
+        const int last_allowed = g.max_cyc + 1;
+        bool converged = false;
+        while (true) {
+          const int b_dst = st.buf[n & 1], b_src = st.buf[(n - 1) & 1];
+          const double* sm = n == 1 ? init_m : tabm(b_src);
+          const double* sc = n == 1 ? init_c : tabc(b_src);
+          const bool track = n >= 2;
+          double dl;
+          if (pk == 1)
+            dl = ge_egm_cycle_fn<SMAX, SC, 1, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                              gam);
+          else if (pk == 3)
+            dl = ge_egm_cycle_fn<SMAX, SC, 3, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                              gam);
+          else if (pk == 5)
+            dl = ge_egm_cycle_fn<SMAX, SC, 5, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                              gam);
+          else
+            dl = ge_egm_cycle_fn<SMAX, SC, 0, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
+                                              gam);
+          // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
+          // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
+          const bool want_value = ext && n >= kGeExtrap - 1 &&
+                                  ((n % kGeExtrap) == kGeExtrap - 1 || (n % kGeExtrap) == 0);
+          double dclu = 0.0;
+          bool go;
+          if (want_value) {
+            double v[1] = {dl};
+            if (!ge_reduce<TH>(gran, G, w, ne, v, 1, 1u, s_part, s_res, &s_flag, g.err)) return;
+            dclu = s_res[0];
+            go = dclu > st.etol;   // NaN: stop (HARK: go = distance > tolerance)
+            if (tid == 0) st.nan_stop = dclu != dclu;
+          } else {
+            const double dw = wave_nan_max(dl);
+            if ((tid & (kWave - 1)) == 0) s_part[0][tid / kWave] = dw;
+            __syncthreads();
+            unsigned flag = 0u;
+            if (tid == 0) {
+              double d = s_part[0][0];
+              for (int q = 1; q < TH / kWave; ++q) d = nan_max(d, s_part[0][q]);
+              flag = (d > st.etol ? 1u : 0u) | (d != d ? (1u << 16) : 0u);
+              ++st.nbc;
             }
-            st.lam_prev = lam;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const unsigned k = st.nbc, par = k & 1u;
+            if (!hc_barrier_count(g.err, &cw[par], (unsigned)G * ((k + par) / 2), flag, &s_nc, &s_flag)) return;
+            if (tid == 0) {
+              const unsigned dlt = s_nc - st.nc_prev[par];
+              st.nc_prev[par] = s_nc;
+              st.stop = (dlt & 0xffffu) == 0u || (dlt >> 16) != 0u;
+              st.nan_stop = (dlt >> 16) != 0u;
+            }
+            __syncthreads();
+            go = !st.stop;
           }
-          __syncthreads();
-          const double f = st.fext;
-          if (f != 0.0) {
-            double* cm = tabm(b_dst);
-            double* cc = tabc(b_dst);
-            const double* pm = tabm(b_src);
-            const double* pc = tabc(b_src);
-            for (int s = 0; s < S; ++s)
-              for (int k = j0 + tid; k < j1; k += TH) {
-                const size_t o = (size_t)s * n1 + k + 1;
-                const double x = load_f64_agent(&cm[o]), y = load_f64_agent(&cc[o]);
-                store_f64_agent(&cm[o], x + f * (x - load_f64_agent(&pm[o])));
-                store_f64_agent(&cc[o], y + f * (y - load_f64_agent(&pc[o])));
+          if (track && !go) {
+            converged = true;
+            break;
+          }
+          if (n >= last_allowed) break;
+          // geometric extrapolation at the checks (ge.hip / egm.hip egm_extrap_kernel)
+          if (want_value && (n % kGeExtrap) == 0) {
+            if (tid == 0) {
+              const double d1 = dclu, d0 = st.dist, lam = d1 / d0;
+              st.fext = 0.0;
+              if (n >= 4 && d1 > 100.0 * st.etol && lam > 0.5 && lam < 0.999 && st.lam_prev > 0.0 &&
+                  fabs(lam - st.lam_prev) < 0.2 * (1.0 - lam)) {
+                st.fext = lam / (1.0 - lam);
+                st.moved = 1;
               }
-            if (!plain_barrier()) return;
+              st.lam_prev = lam;
+            }
+            __syncthreads();
+            const double f = st.fext;
+            if (f != 0.0) {
+              double* cm = tabm(b_dst);
+              double* cc = tabc(b_dst);
+              const double* pm = tabm(b_src);
+              const double* pc = tabc(b_src);
+              for (int s = 0; s < S; ++s)
+                for (int k = j0 + tid; k < j1; k += TH) {
+                  const size_t o = (size_t)s * n1 + k + 1;
+                  const double x = load_f64_agent(&cm[o]), y = load_f64_agent(&cc[o]);
+                  store_f64_agent(&cm[o], x + f * (x - load_f64_agent(&pm[o])));
+                  store_f64_agent(&cc[o], y + f * (y - load_f64_agent(&pc[o])));
+                }
+              if (!plain_barrier()) return;
+            }
+          } else if (want_value) {
+            if (tid == 0) st.dist = dclu;
           }
-        } else if (want_value) {
-          if (tid == 0) st.dist = dclu;
+          ++n;
         }
-        ++n;
+        if (tid == 0) {
+          st.n = n;
+          if (!converged) st.status |= 1;
+        }
+        __syncthreads();
+        final_buf = st.buf[n & 1];
+        // an extrapolated solve that ended in NaN: the whole solve again, plain (ge.hip)
+        if (!(st.moved && st.nan_stop)) break;
+        if (tid == 0) {
+          st.extrap = 0;
+          st.status &= ~1;
+        }
+        __syncthreads();
       }
       if (tid == 0) {
-        st.n = n;
-        if (!converged) st.status |= 1;
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        st.t_egm += tn - tp;
+        st.cyc_sum += st.n;
+        // buffer roles: prev <- cur, cur <- the solve's final tables, the freed ones ping-pong
+        const int fb = final_buf;
+        const int other = st.buf[0] == fb ? st.buf[1] : st.buf[0];
+        const int old_prev = st.buf[3];
+        st.buf[3] = st.buf[2];
+        st.buf[2] = fb;
+        st.buf[0] = other;
+        st.buf[1] = old_prev;
       }
       __syncthreads();
-      final_buf = st.buf[n & 1];
-      // an extrapolated solve that ended in NaN: the whole solve again, plain (ge.hip)
-      if (!(st.moved && st.nan_stop)) break;
+      // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
+      tp = __builtin_amdgcn_s_memrealtime();
+      ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
+      // ---- the distribution's start (own columns) ----
+      if (st.fresh_mass) {
+        const double u0 = 1.0 / ((double)S * n_a);
+        for (int s = 0; s < S; ++s)
+          for (int k = j0 + tid; k < j1; k += TH) X[(size_t)s * n_a + k] = u0;
+      } else if (warm) {
+        for (int s = 0; s < S; ++s)
+          for (int k = j0 + tid; k < j1; k += TH) {
+            const size_t o = (size_t)s * n_a + k;
+            const double x = X[o];
+            if (secant) X[o] = theta == 0.0 ? x : x + theta * (x - PX[o]);
+            PX[o] = x;
+          }
+      }
+      __syncthreads();
       if (tid == 0) {
-        st.extrap = 0;
-        st.status &= ~1;
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        st.t_lot += tn - tp;
+        tp = tn;
       }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-      st.t_egm += tn - tp;
-      st.cyc_sum += st.n;
-      // buffer roles: prev <- cur, cur <- the solve's final tables, the freed ones ping-pong
-      const int fb = final_buf;
-      const int other = st.buf[0] == fb ? st.buf[1] : st.buf[0];
-      const int old_prev = st.buf[3];
-      st.buf[3] = st.buf[2];
-      st.buf[2] = fb;
-      st.buf[0] = other;
-      st.buf[1] = old_prev;
-    }
-    __syncthreads();
-    // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
-    tp = __builtin_amdgcn_s_memrealtime();
-    ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
-    // ---- the distribution's start (own columns) ----
-    if (st.fresh_mass) {
-      const double u0 = 1.0 / ((double)S * n_a);
-      for (int s = 0; s < S; ++s)
-        for (int k = j0 + tid; k < j1; k += TH) X[(size_t)s * n_a + k] = u0;
-    } else if (warm) {
-      for (int s = 0; s < S; ++s)
-        for (int k = j0 + tid; k < j1; k += TH) {
-          const size_t o = (size_t)s * n_a + k;
-          const double x = X[o];
-          if (secant) X[o] = theta == 0.0 ? x : x + theta * (x - PX[o]);
-          PX[o] = x;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-      st.t_lot += tn - tp;
-      tp = tn;
     }
     // ---- the stationary distribution: BiCGSTAB on (I - T) mass = 0 ----
     int mv;
@@ -717,14 +724,26 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.ctr = to_global(ctr); hk.gran = to_global(gran); hk.Pc = to_global(g.P + (size_t)cal * S * S);
       hk.max_iter = g.max_hist; hk.err = to_global(g.err);
       hk.tol = st.htol;
+      hk.stop_ctr = to_global((const unsigned*)(g.stop_at > 0 ? g.done_ctr : nullptr));
+      hk.stop_at = (unsigned)g.stop_at;
       mv = hk_solve_isolated<SMAX, KC, TH>(hk, &nb, &ne);
     }
-    if (mv < 0) return;
+    if (mv == -1) return;
     if (tid == 0) {
       const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
       st.t_hist += tn - tp;
       tp = tn;
     }
+    if (mv <= -2) {   // rebalancing stop inside the solve: resume it in the next launch
+      if (tid == 0) {
+        st.its_sum += -mv - 2;
+        st.in_hist = 1;
+      }
+      __syncthreads();
+      stopped = true;
+      break;
+    }
+    if (tid == 0) st.in_hist = 0;
     // ---- K_s = sum mass a over the cluster ----
     double part = 0.0;
     for (int k = j0 + tid; k < j1; k += TH) {

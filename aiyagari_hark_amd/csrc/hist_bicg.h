@@ -11,6 +11,7 @@ namespace aiy {
 
 constexpr int kHkRed = 8;   // partial sums per reduction (at most)
 constexpr int kHkStall = 256;   // matvecs without a 10 % residual gain that count as a stall
+constexpr double kHkStopSentinel = 1e300;   // rebalancing stop request on the max|r| partial
 static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
@@ -79,10 +80,16 @@ struct HkArgs {
   double tol;
   int max_iter;
   gptr<unsigned> err;
+  // rebalancing (ge_resident.hip): stop at the next iteration once *stop_ctr >= stop_at
+  // (nullptr: never); the solve then returns -(2 + matvecs) with X a valid iterate
+  gptr<const unsigned> stop_ctr;
+  unsigned stop_at;
 };
 
 // Returns the matvecs of the solve, or -1 when the cluster stops (error word set: a
-// timeout, a span that does not fit, too many covering workgroups).  nb / ne: the
+// timeout, a span that does not fit, too many covering workgroups), or -(2 + matvecs) when
+// a rebalancing stop was requested (X holds the current iterate; a later solve restarts
+// from it).  nb / ne: the
 // cluster barriers / reductions passed so far in this launch (counted on).
 template <int SMAX, int KC, int TH>
 __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
@@ -566,6 +573,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     for (int k = 0; k < KC; ++k)
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) Vl[vidx(k, s)] = rv[k][s];
+    // rebalancing stop request: polled every 8th iteration by thread 0 into LDS (the matvec's
+    // barriers make it visible; the partial below carries it to every workgroup)
+    if (r.stop_ctr != nullptr && tid == 0 && (mv & 15) == 0)
+      s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
     if (!matvec(pv, tv)) return -1;
     ++mv;
     int jc = col();
@@ -583,7 +594,9 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         }
       }
     part[0] = rvv;
-    part[1] = rm;
+    // the stop request rides on the max|r| partial as a sentinel no residual of a mass vector
+    // reaches (the cluster max is the same in every workgroup)
+    part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
     double xq[KC][SMAX];   // x of the own points, for x += alpha p
     if (!reduce(part, 2, 2u, [&] {
           const int jq = col();
@@ -593,6 +606,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
         }))
       return -1;
+    if (s_res[1] >= kHkStopSentinel) return -(2 + mv);   // every workgroup reads the same max
     if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
       restart = true;
       continue;

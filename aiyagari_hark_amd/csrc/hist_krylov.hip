@@ -76,6 +76,8 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   a.tol = r.tolv ? r.tolv[cal] : r.tol;
   a.max_iter = r.max_iter;
   a.err = to_global(r.err);
+  a.stop_ctr = to_global((const unsigned*)nullptr);
+  a.stop_at = 0u;
   unsigned nb = 0, ne = 0;
   const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
