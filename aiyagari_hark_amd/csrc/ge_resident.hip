@@ -52,7 +52,7 @@ constexpr int kGeTHMax = 1024;
 constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
-constexpr int kGeExtrap = 32;             // cycles between extrapolation checks (ge.hip's host chunk)
+constexpr int kGeExtrap = 32;             // default cycles between extrapolation checks (ge.hip's host chunk)
 template <int NW>
 constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
 
@@ -73,6 +73,7 @@ struct GeRun {
   double r_tol, egm_tol, hist_tol;
   int max_steps, max_cyc, max_hist;
   int warm_hist, warm_egm, secant, loose, extrap;
+  int extrap_period;      // EGM cycles between extrapolation checks (>= 4)
   double* tab;            // [n_cal][kGeBufs][2][S][n_a + 1]
   double* mass;           // [n_cal][S][n_a]
   double* pmass;          // [n_cal][S][n_a] previous evaluation's mass
@@ -588,8 +589,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
                                               gam);
           // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
           // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
-          const bool want_value = ext && n >= kGeExtrap - 1 &&
-                                  ((n % kGeExtrap) == kGeExtrap - 1 || (n % kGeExtrap) == 0);
+          const int xp = g.extrap_period;
+          const bool want_value = ext && n >= xp - 1 && ((n % xp) == xp - 1 || (n % xp) == 0);
           double dclu = 0.0;
           bool go;
           if (want_value) {
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
           }
           if (n >= last_allowed) break;
           // geometric extrapolation at the checks (ge.hip / egm.hip egm_extrap_kernel)
-          if (want_value && (n % kGeExtrap) == 0) {
+          if (want_value && (n % xp) == 0) {
             if (tid == 0) {
               const double d1 = dclu, d0 = st.dist, lam = d1 / d0;
               st.fext = 0.0;
@@ -930,6 +931,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.max_hist = o->max_hist_iter > 0 ? o->max_hist_iter : 200000;
   g.warm_hist = o->warm_hist != 0; g.warm_egm = o->warm_egm != 0;
   g.secant = o->secant_start != 0; g.loose = o->loose_bracket != 0; g.extrap = o->egm_extrapolate != 0;
+  g.extrap_period = h->ge_extrap_period;
   g.tab = reinterpret_cast<double*>(base + L.tab);
   g.mass = reinterpret_cast<double*>(base + L.mass);
   g.pmass = reinterpret_cast<double*>(base + L.pmass);

@@ -352,6 +352,8 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     stops every cluster at an evaluation boundary once q % of a
                                     launch's calibrations have finished and relaunches the rest on
                                     the freed compute units (larger clusters); 0: one launch */
+#define AIY_OPT_GE_EXTRAP_PERIOD 13 /* device-resident GE search: EGM cycles between the geometric
+                                    extrapolation checks (4 .. 1024; default 32) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

@@ -31,6 +31,9 @@ for step in "$@"; do
     q34) run q34 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 34 ;;
     q67) run q67 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 67 ;;
     q80) run q80 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 80 ;;
+    x4) run x4 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 4 ;;
+    x8) run x8 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 8 ;;
+    x16) run x16 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 16 ;;
     g24off) run g24off 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 0 ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
