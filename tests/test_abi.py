@@ -104,3 +104,15 @@ def test_panel_table_bytes_host_only(lib):
     assert lib.aiy_panel_table_bytes(7, 15, 1, 0) == -1
     assert lib.aiy_panel_table_bytes(0, 15, 32, 0) == -1
     assert lib.aiy_panel_table_bytes(17, 15, 32, 0) == -1
+
+
+def test_option_constants_match_header():
+    """Every AIY_OPT_* the header defines has the same value in the Python binding
+    (aiyagari_hark_amd._lib), so aiy_set_option calls from Python mean what the C side reads."""
+    import re
+    from aiyagari_hark_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "aiyagari.h")).read()
+    opts = dict((k, int(v)) for k, v in re.findall(r"#define (AIY_OPT_[A-Z0-9_]+) (\d+)", hdr))
+    assert "AIY_OPT_GE_REBALANCE" in opts and "AIY_OPT_GE_EXTRAP_PERIOD" in opts
+    for k, v in opts.items():
+        assert getattr(_lib, k) == v, k
