@@ -143,6 +143,7 @@ SIGNATURES = {
     "aiy_hist_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]),
     "aiy_ge_resident_plan": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_int32_p]),
     "aiy_ge_last_profile": (ctypes.c_int32, [vp, c_double_p, ctypes.c_int32]),
+    "aiy_ge_last_eval_log": (ctypes.c_int32, [vp, c_double_p, ctypes.c_int32]),
     "aiy_ge_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), c_double_p, c_double_p,
                                              ctypes.c_int32]),
     "aiy_ge_stationary_work_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),

@@ -102,10 +102,14 @@ struct GeRun {
   int* out_its;
   int* out_status;
   double* out_prof;       // [n_cal][kGeProf] workgroup 0's phase times (us) and counts
+  double* out_evlog;      // [n_cal][kGeEvLog][kGeEvRec] per-evaluation record (measurement)
 };
 // per-calibration profile of the launch (workgroup 0, s_memrealtime at 100 MHz): EGM, lottery,
 // distribution solve, K reduction + search, whole search (us); EGM cycles, matvecs, evaluations
 constexpr int kGeProf = 8;
+// per-evaluation log: r, (K_s - K_d) / K_d, EGM cycles, matvecs, loose, EGM + histogram us
+constexpr int kGeEvLog = 32;
+constexpr int kGeEvRec = 6;
 
 // Search state of one calibration, one copy per workgroup (thread 0 writes, all read).
 struct GeState {
@@ -115,7 +119,7 @@ struct GeState {
   int in_hist;             // stopped (rebalancing) inside this evaluation's distribution solve
   int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
   long long cyc_sum, its_sum;
-  unsigned long long t_egm, t_lot, t_hist, t_k, t0;
+  unsigned long long t_egm, t_lot, t_hist, t_k, t0, t_ev0;
   unsigned nc_prev[2];
   unsigned nbc;            // counting barriers passed
 };
@@ -507,6 +511,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     // a calibration stopped inside its distribution solve resumes there (prices, tables,
     // lottery and the iterate are in the saved state and HBM)
     unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && !st.in_hist) st.t_ev0 = tp;
     if (!st.in_hist) {
       // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
       if (tid == 0) {
@@ -758,6 +763,15 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     }
     if (tid == 0) {
       const double Ks = s_res[0];
+      if (w == 0 && st.steps < kGeEvLog) {
+        double* ev = g.out_evlog + ((size_t)cal * kGeEvLog + st.steps) * kGeEvRec;
+        ev[0] = st.rs.x;
+        ev[1] = (Ks - st.Kd) / st.Kd;
+        ev[2] = (double)st.n;
+        ev[3] = (double)mv;
+        ev[4] = (double)st.loose;
+        ev[5] = (double)(__builtin_amdgcn_s_memrealtime() - st.t_ev0) * 0.01;
+      }
       st.its_sum += mv;
       if (mv >= g.max_hist) st.status |= 2;
       st.r_prev = st.r_cur;
@@ -857,7 +871,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 
 struct GeScratch {
   size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
-      bytes;
+      evlog, bytes;
 };
 // Per-calibration arrays (kept across the rebalancing launches) first, then the per-launch
 // cluster arrays sized for the most workgroups any launch can hold (cus) and the largest span
@@ -883,6 +897,7 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_m
   L.outd = take((size_t)n_cal * 3 * sizeof(double));
   L.outi = take((size_t)n_cal * 4 * sizeof(int));
   L.prof = take((size_t)n_cal * kGeProf * sizeof(double));
+  L.evlog = take((size_t)n_cal * kGeEvLog * kGeEvRec * sizeof(double));
   L.bytes = o;
   return L;
 }
@@ -955,6 +970,8 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.out_r = outd; g.out_K = outd + n_cal; g.out_Ks = outd + 2 * n_cal;
   g.out_steps = outi; g.out_cyc = outi + n_cal; g.out_its = outi + 2 * n_cal; g.out_status = outi + 3 * n_cal;
   g.out_prof = reinterpret_cast<double*>(base + L.prof);
+  g.out_evlog = reinterpret_cast<double*>(base + L.evlog);
+  AIY_HIP(h, hipMemsetAsync(g.out_evlog, 0, (size_t)n_cal * kGeEvLog * kGeEvRec * sizeof(double), st));
   AIY_HIP(h, hipMemcpyAsync(base + L.cal, cals.data(), sizeof(GeCalDev) * n_cal, hipMemcpyHostToDevice, st));
   AIY_HIP(h, hipMemsetAsync(d_resume, 0, (size_t)n_cal * sizeof(int), st));
   AIY_HIP(h, hipMemsetAsync(g.out_done, 0, (size_t)n_cal * sizeof(int), st));
@@ -1020,6 +1037,9 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   AIY_HIP(h, hipMemcpyAsync(hd.data(), outd, sizeof(double) * 3 * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(hi.data(), outi, sizeof(int) * 4 * n_cal, hipMemcpyDeviceToHost, st));
   h->ge_prof.assign((size_t)n_cal * kGeProf, 0.0);
+  h->ge_evlog.assign((size_t)n_cal * kGeEvLog * kGeEvRec, 0.0);
+  AIY_HIP(h, hipMemcpyAsync(h->ge_evlog.data(), g.out_evlog, sizeof(double) * kGeEvLog * kGeEvRec * n_cal,
+                            hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipMemcpyAsync(h->ge_prof.data(), g.out_prof, sizeof(double) * kGeProf * n_cal, hipMemcpyDeviceToHost,
                             st));
   AIY_HIP(h, hipStreamSynchronize(st));
@@ -1074,6 +1094,20 @@ extern "C" int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* l
     h->ge_egm_cycles = 0.0;
   }
   return AIY_OK;
+}
+
+// Per-evaluation log of the last device-resident search (measurement hook): out[(c * 32 + e)
+// * 6 + k] for evaluation e of calibration c, k = r, (K_s - K_d) / K_d, EGM cycles, matvecs,
+// loose (1: a bracketing evaluation at the loose tolerances), microseconds from the
+// evaluation's start (workgroup 0's clock; a solve split by a rebalancing stop includes the
+// relaunch gap, its matvecs count the resumed part only); rows past
+// a calibration's evaluations are zero.  Returns the calibrations written.  Host-only.
+extern "C" int32_t aiy_ge_last_eval_log(aiy_handle* h, double* out, int32_t n_cal) {
+  if (!h || !out || n_cal < 0) return AIY_ERR_ARG;
+  const int have = (int)(h->ge_evlog.size() / (kGeEvLog * kGeEvRec));
+  const int n = std::min(have, (int)n_cal);
+  std::copy(h->ge_evlog.begin(), h->ge_evlog.begin() + (size_t)n * kGeEvLog * kGeEvRec, out);
+  return n;
 }
 
 // Per-calibration profile of the last device-resident GE launch (measurement hook):

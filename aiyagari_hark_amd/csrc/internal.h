@@ -67,6 +67,7 @@ struct aiy_handle {
   double ge_ms_sum = 0.0, ge_points = 0.0, ge_egm_cycles = 0.0;
   long long ge_launches = 0;
   std::vector<double> ge_prof;       // [n_cal][8] per-calibration profile of the last launch
+  std::vector<double> ge_evlog;      // [n_cal][32][6] per-evaluation log of the last search
   // wealth statistics (stats.hip): sort / scan scratch
   void* d_stats = nullptr;
   size_t stats_cap = 0;

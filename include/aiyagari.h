@@ -462,6 +462,9 @@ int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, do
  * (microseconds, workgroup 0's clock), EGM cycles, matvecs, evaluations.  Returns the
  * calibrations written (<= n_cal).  Host-only. */
 int32_t aiy_ge_last_profile(aiy_handle* h, double* out, int32_t n_cal);
+/* Per-evaluation log of the last device-resident search: out[(c * 32 + e) * 6 + k], k = r,
+   (K_s - K_d) / K_d, EGM cycles, matvecs, loose flag, microseconds (measurement hook). */
+int32_t aiy_ge_last_eval_log(aiy_handle* h, double* out, int32_t n_cal);
 
 /* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
  * the device-resident distribution-iteration launches since the last reset (HIP events on

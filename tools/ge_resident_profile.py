@@ -72,6 +72,17 @@ def main():
                       f"({int(mv):5d} mv, {hist / max(1, mv):5.2f} us)  K {k / 1e3:5.2f} ms  evals {int(ev)}",
                       file=sys.stderr, flush=True)
             out["profile"] = rows
+            ev = (ctypes.c_double * (32 * 6 * len(cals)))()
+            ne = h.lib.aiy_ge_last_eval_log(h.h, ev, len(cals))
+            e = np.array(ev[:32 * 6 * ne]).reshape(ne, 32, 6)
+            out["evaluations"] = [[dict(r=float(x[0]), f_rel=float(x[1]), egm_cycles=int(x[2]), matvecs=int(x[3]),
+                                        loose=int(x[4]), us=round(float(x[5]), 1)) for x in e[c] if x[2] > 0]
+                                  for c in range(ne)]
+            for c in (0, 11, 23):
+                if c < ne:
+                    print(f"[evals] cell {c}: " + "; ".join(f"r={x['r']:.6f} f={x['f_rel']:+.1e} cyc={x['egm_cycles']} "
+                                                            f"mv={x['matvecs']}{' L' if x['loose'] else ''}"
+                                                            for x in out["evaluations"][c]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 
 
