@@ -74,6 +74,7 @@ struct GeRun {
   int max_steps, max_cyc, max_hist;
   int warm_hist, warm_egm, secant, loose, extrap;
   int extrap_period;      // EGM cycles between extrapolation checks (>= 4)
+  int logsec;             // log-secant bracketing (AIY_OPT_GE_LOGSEC, with loose bracketing)
   double* tab;            // [n_cal][kGeBufs][2][S][n_a + 1]
   double* mass;           // [n_cal][S][n_a]
   double* pmass;          // [n_cal][S][n_a] previous evaluation's mass
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st = g.saved[cal];
       st.t0 = __builtin_amdgcn_s_memrealtime() - st.t0;   // saved: the time spent so far
     } else {
-      st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method);
+      st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method, g.loose && g.logsec);
       st.r_cur = st.r_prev = 0.0;
       st.Ks = 0.0;
       st.steps = 0;
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st.r_cur = st.rs.x;
       const double f = Ks - st.Kd;
       st.refine = st.loose && !(fabs(f) >= kGeSignMargin * st.Kd);   // NaN: refine
-      if (!st.refine) st.rs.update(f);
+      if (!st.refine) st.rs.update(f, st.Kd);
       st.Ks = Ks;
       ++st.steps;
       st.t_k += __builtin_amdgcn_s_memrealtime() - tp;
@@ -947,6 +948,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.warm_hist = o->warm_hist != 0; g.warm_egm = o->warm_egm != 0;
   g.secant = o->secant_start != 0; g.loose = o->loose_bracket != 0; g.extrap = o->egm_extrapolate != 0;
   g.extrap_period = h->ge_extrap_period;
+  g.logsec = h->ge_logsec;
   g.tab = reinterpret_cast<double*>(base + L.tab);
   g.mass = reinterpret_cast<double*>(base + L.mass);
   g.pmass = reinterpret_cast<double*>(base + L.pmass);

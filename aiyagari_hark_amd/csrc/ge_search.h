@@ -14,6 +14,17 @@ namespace aiy {
 struct RootSearch {
   double lo, hi, xtol;
   bool have_lo, have_hi, brent, done;
+  // log-secant bracketing (with loose bracketing): while only K_s < K_d has been seen, the
+  // next point comes from a secant of g = log(K_s / K_d) against u = log(rtop - r) through
+  // the last two such points -- near 1/beta - 1 the excess supply grows about exponentially
+  // in u -- aimed 20 % past the predicted root, its distance to rtop kept within [1/16, 1/2]
+  // of the current one (1/2: bisection toward rtop)
+  // ... and Brent's method then runs in the same coordinates (u, g), where the root is nearly
+  // linear, with the tolerance xtol / (rtop - lo) in u (so the bracket in r is <= xtol)
+  bool logsec;
+  int nneg;
+  double rtop, ua, ga, ub, gb, glo, ghi;
+  bool logb;   // Brent runs in (u, g)
   double flo, fhi, x;
   double xpre, fpre, xcur, fcur, xblk, fblk, spre, scur;
   double xprev_eval, fprev_eval;
@@ -22,8 +33,13 @@ struct RootSearch {
   __host__ __device__ static double fabs_(double v) { return v < 0 ? -v : v; }
   __host__ __device__ static double fmin_(double a, double b) { return (b < a) ? b : a; }   // std::min
 
-  __host__ __device__ void init(double l, double h, double tol, int meth) {
+  __host__ __device__ void init(double l, double h, double tol, int meth, bool log_secant = false) {
     lo = l; hi = h; xtol = tol; method = meth;
+    logsec = log_secant && meth == 1;
+    nneg = 0;
+    rtop = h;
+    ua = ga = ub = gb = glo = ghi = 0.0;
+    logb = false;
     have_lo = have_hi = brent = false;
     flo = fhi = 0.0;
     xpre = fpre = xcur = fcur = xblk = fblk = spre = scur = 0.0;
@@ -31,7 +47,7 @@ struct RootSearch {
     x = 0.5 * (lo + hi);
     done = !(hi - lo > xtol);
   }
-  __host__ __device__ void update(double f) {
+  __host__ __device__ void update(double f, double Kd = 0.0) {
     if (done) return;
     if (method == 0) {   // oracle ge_bisect: Ks > Kd -> hi = mid
       if (f > 0) hi = x; else lo = x;
@@ -39,18 +55,44 @@ struct RootSearch {
       x = 0.5 * (lo + hi);
       return;
     }
+    const bool tr = logsec && Kd > 0 && f > -Kd;   // transformed coordinates available
     if (!brent) {
       if (f > 0) { hi = x; fhi = f; have_hi = true; } else { lo = x; flo = f; have_lo = true; }
+      if (tr) (f > 0 ? ghi : glo) = log1p(f / Kd);
       if (hi - lo <= xtol) { done = true; x = 0.5 * (lo + hi); return; }
-      if (!have_lo || !have_hi) { x = 0.5 * (lo + hi); return; }
+      if (!have_lo || !have_hi) {
+        const double xe = x;
+        x = 0.5 * (lo + hi);
+        if (logsec && !have_hi && Kd > 0 && f > -Kd && xe < rtop) {
+          ua = ub; ga = gb;
+          ub = log(rtop - xe); gb = log1p(f / Kd);
+          if (++nneg >= 2 && gb > ga && ub < ua) {
+            const double us = ub - gb * (ub - ua) / (gb - ga);   // predicted root in u
+            const double dc = rtop - xe;
+            double dn = 0.8 * exp(us);
+            dn = dn < dc / 16 ? dc / 16 : (dn > dc / 2 ? dc / 2 : dn);
+            const double xn = rtop - dn;
+            if (xn > lo && xn < hi) x = xn;
+          }
+        }
+        return;
+      }
       brent = true;
-      xpre = lo; fpre = flo; xcur = hi; fcur = fhi;
+      if (logsec && tr && hi < rtop) {   // Brent in (u, g); xtol in u keeps the r bracket <= xtol
+        logb = true;
+        xtol = xtol / (rtop - lo);
+        xpre = log(rtop - lo); fpre = glo; xcur = log(rtop - hi); fcur = ghi;
+      } else {
+        xpre = lo; fpre = flo; xcur = hi; fcur = fhi;
+      }
       xblk = fblk = spre = scur = 0.0;
       step();
+      if (logb) x = rtop - exp(x);
       return;
     }
-    xpre = xprev_eval; fpre = fprev_eval; fcur = f;
+    xpre = xprev_eval; fpre = fprev_eval; fcur = logb ? (tr ? log1p(f / Kd) : (f > 0 ? 1e300 : -1e300)) : f;
     step();
+    if (logb) x = rtop - exp(x);
   }
   __host__ __device__ void step() {
     const double kEps = 2.220446049250313e-16;   // DBL_EPSILON

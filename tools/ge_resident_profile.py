@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--modes", default="resident,host")
     ap.add_argument("--rebalance", type=int, default=-1, help="AIY_OPT_GE_REBALANCE (-1: default)")
     ap.add_argument("--extrap", type=int, default=-1, help="AIY_OPT_GE_EXTRAP_PERIOD (-1: default)")
+    ap.add_argument("--logsec", type=int, default=-1, help="AIY_OPT_GE_LOGSEC (-1: default)")
     args = ap.parse_args()
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
@@ -40,6 +41,8 @@ def main():
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, args.cluster_cap), "opt")
     if args.rebalance >= 0:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, args.rebalance), "opt")
+    if args.logsec >= 0:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOGSEC, args.logsec), "opt")
     if args.extrap >= 0:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_EXTRAP_PERIOD, args.extrap), "opt")
     out = {}

@@ -34,6 +34,8 @@ for step in "$@"; do
     x4) run x4 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 4 ;;
     x8) run x8 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 8 ;;
     x16) run x16 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --extrap 16 ;;
+    ls0) run ls0 300 python -u tools/ge_resident_profile.py --modes resident,host --reps 3 --logsec 0 ;;
+    g24h) run g24h 300 python -u tools/ge_resident_profile.py --modes resident,host --reps 3 ;;
     g24off) run g24off 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 0 ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
