@@ -417,7 +417,10 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     (else that r is evaluated again at the full tolerances).  The two bracket endpoints
     Brent's method starts from may be such loose evaluations (their sign is certain, their
     value good to ~1e-6 relative); every later point is a full-tolerance evaluation, and
-    the root is still bracketed by the 5 % sign margin.  extrapolate (native only;
+    the root is still bracketed by the 5 % sign margin.  With loose bracketing the native
+    search also brackets and runs Brent's method in log coordinates (log K_s/K_d against
+    log(1/beta - 1 - r), where the excess supply is nearly linear; AIY_OPT_GE_LOGSEC,
+    csrc/ge_search.h): the same root to r_tol in fewer evaluations.  extrapolate (native only;
     default: on for "brent"): the household solves extrapolate their cycle iterates
     geometrically where the distances fall at a steady rate (csrc/egm.hip; same stopping
     rule).  groups (native only; default: 3 for "brent" with >= 3 calibrations, else 1):
