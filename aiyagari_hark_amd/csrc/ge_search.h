@@ -3,13 +3,20 @@
 // method 0 = bisection (oracle/stationary.py ge_bisect, step for step); method 1 =
 // bisection until both signs of f are evaluated, then Brent's method (the
 // scipy.optimize.brentq algorithm; aiyagari_hark_amd/stationary.py _Brent is the same
-// coroutine in Python).  Every workgroup of a device cluster runs its own copy on
-// bit-identical inputs, so all copies take the same steps.
+// coroutine in Python), or -- with loose bracketing -- the log-coordinate bracketing and
+// Brent described at `logsec` below (no Python mirror: the Python engine runs without loose
+// bracketing).  Every workgroup of a device cluster runs its own copy on bit-identical
+// inputs, so all copies take the same steps.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 namespace aiy {
+
+#ifndef AIY_GE_LOGSEC_FIRST
+#define AIY_GE_LOGSEC_FIRST 1
+#endif
+constexpr bool kGeLogsecFirst = AIY_GE_LOGSEC_FIRST != 0;   // log-secant step from one point
 
 struct RootSearch {
   double lo, hi, xtol;
@@ -66,8 +73,12 @@ struct RootSearch {
         if (logsec && !have_hi && Kd > 0 && f > -Kd && xe < rtop) {
           ua = ub; ga = gb;
           ub = log(rtop - xe); gb = log1p(f / Kd);
-          if (++nneg >= 2 && gb > ga && ub < ua) {
-            const double us = ub - gb * (ub - ua) / (gb - ga);   // predicted root in u
+          ++nneg;
+          // one point: the slope dg/du = -1 the Table II cells show far from 1/beta - 1
+          // (K_s / K_d - 1 about doubles per halving of the distance); two: their secant
+          const bool two = nneg >= 2 && gb > ga && ub < ua;
+          if (two || (nneg == 1 && kGeLogsecFirst)) {
+            const double us = two ? ub - gb * (ub - ua) / (gb - ga) : ub + gb;   // predicted root in u
             const double dc = rtop - xe;
             double dn = 0.8 * exp(us);
             dn = dn < dc / 16 ? dc / 16 : (dn > dc / 2 ? dc / 2 : dn);
