@@ -70,6 +70,16 @@ struct RootSearch {
       if (!have_lo || !have_hi) {
         const double xe = x;
         x = 0.5 * (lo + hi);
+        if (logsec && !have_lo && tr && f > 0 && xe < rtop) {
+          // only K_s > K_d seen (the first point was above the root): the same unit-slope
+          // prediction from the latest point, aimed 25 % beyond the root (away from rtop),
+          // the distance to rtop grown 2 .. 16 times; bisection if that leaves the bracket
+          const double dc = rtop - xe;
+          double dn = 1.25 * exp(log(dc) + log1p(f / Kd));
+          dn = dn < 2 * dc ? 2 * dc : (dn > 16 * dc ? 16 * dc : dn);
+          const double xn = rtop - dn;
+          if (xn > lo && xn < hi) x = xn;
+        }
         if (logsec && !have_hi && Kd > 0 && f > -Kd && xe < rtop) {
           ua = ub; ga = gb;
           ub = log(rtop - xe); gb = log1p(f / Kd);
