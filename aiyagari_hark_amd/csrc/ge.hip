@@ -149,7 +149,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   for (int c = 0; c < n_cal; ++c) {
     const double lo0 = o->r_lo ? o->r_lo[c] : -0.5 * M->delta[c];
     const double hi0 = o->r_hi ? o->r_hi[c] : 1.0 / M->disc[c] - 1.0 - 1e-9;
-    rs[c].init(lo0, hi0, o->r_tol, o->method, o->loose_bracket != 0 && h->ge_logsec);
+    rs[c].init(lo0, hi0, o->r_tol, o->method, o->loose_bracket != 0 ? h->ge_logsec : 0);
   }
   std::vector<double> R(n_cal), w(n_cal), Kd(n_cal), Ks(n_cal, 0.0);
   std::vector<int32_t> cyc(n_cal), its(n_cal);

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st = g.saved[cal];
       st.t0 = __builtin_amdgcn_s_memrealtime() - st.t0;   // saved: the time spent so far
     } else {
-      st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method, g.loose && g.logsec);
+      st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method, g.loose ? g.logsec : 0);
       st.r_cur = st.r_prev = 0.0;
       st.Ks = 0.0;
       st.steps = 0;

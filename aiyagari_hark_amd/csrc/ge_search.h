@@ -13,10 +13,6 @@
 
 namespace aiy {
 
-#ifndef AIY_GE_LOGSEC_FIRST
-#define AIY_GE_LOGSEC_FIRST 1
-#endif
-constexpr bool kGeLogsecFirst = AIY_GE_LOGSEC_FIRST != 0;   // log-secant step from one point
 
 struct RootSearch {
   double lo, hi, xtol;
@@ -28,7 +24,7 @@ struct RootSearch {
   // of the current one (1/2: bisection toward rtop)
   // ... and Brent's method then runs in the same coordinates (u, g), where the root is nearly
   // linear, with the tolerance xtol / (rtop - lo) in u (so the bracket in r is <= xtol)
-  bool logsec;
+  bool logsec, logsec1;   // logsec1: also the one-point step (log_secant == 2)
   int nneg;
   double rtop, ua, ga, ub, gb, glo, ghi;
   bool logb;   // Brent runs in (u, g)
@@ -40,9 +36,10 @@ struct RootSearch {
   __host__ __device__ static double fabs_(double v) { return v < 0 ? -v : v; }
   __host__ __device__ static double fmin_(double a, double b) { return (b < a) ? b : a; }   // std::min
 
-  __host__ __device__ void init(double l, double h, double tol, int meth, bool log_secant = false) {
+  __host__ __device__ void init(double l, double h, double tol, int meth, int log_secant = 0) {
     lo = l; hi = h; xtol = tol; method = meth;
-    logsec = log_secant && meth == 1;
+    logsec = log_secant > 0 && meth == 1;
+    logsec1 = logsec && log_secant >= 2;
     nneg = 0;
     rtop = h;
     ua = ga = ub = gb = glo = ghi = 0.0;
@@ -70,7 +67,7 @@ struct RootSearch {
       if (!have_lo || !have_hi) {
         const double xe = x;
         x = 0.5 * (lo + hi);
-        if (logsec && !have_lo && tr && f > 0 && xe < rtop) {
+        if (logsec1 && !have_lo && tr && f > 0 && xe < rtop) {
           // only K_s > K_d seen (the first point was above the root): the same unit-slope
           // prediction from the latest point, aimed 25 % beyond the root (away from rtop),
           // the distance to rtop grown 2 .. 16 times; bisection if that leaves the bracket
@@ -87,9 +84,11 @@ struct RootSearch {
           // one point: the slope dg/du = -1 the Table II cells show far from 1/beta - 1
           // (K_s / K_d - 1 about doubles per halving of the distance); two: their secant
           const bool two = nneg >= 2 && gb > ga && ub < ua;
-          if (two || (nneg == 1 && kGeLogsecFirst)) {
-            const double us = two ? ub - gb * (ub - ua) / (gb - ga) : ub + gb;   // predicted root in u
-            const double dc = rtop - xe;
+          // (the one-point prediction only where it lies well toward rtop, < 1/4 of the current
+          // distance: the slope is steeper where the root is far below 1/beta - 1)
+          const double us = two ? ub - gb * (ub - ua) / (gb - ga) : ub + gb;   // predicted root in u
+          const double dc = rtop - xe;
+          if (two || (nneg == 1 && logsec1 && exp(us) < dc / 4)) {
             double dn = 0.8 * exp(us);
             dn = dn < dc / 16 ? dc / 16 : (dn > dc / 2 ? dc / 2 : dn);
             const double xn = rtop - dn;

@@ -61,7 +61,7 @@ struct aiy_handle {
   int ge_rebalance = 50;             // AIY_OPT_GE_REBALANCE: % finished that stops a launch (0: one launch)
   int ge_rounds = 0;                 // launches of the last device-resident search
   int ge_extrap_period = 32;         // AIY_OPT_GE_EXTRAP_PERIOD: EGM cycles between extrapolation checks
-  bool ge_logsec = true;             // AIY_OPT_GE_LOGSEC: log-secant bracketing (with loose bracketing)
+  int ge_logsec = 2;                 // AIY_OPT_GE_LOGSEC: 0 off, 1 two-point log-secant bracketing, 2 also from one point (with loose bracketing)
   void* d_ge = nullptr;              // tables, masses, lottery, cluster sync of the launch
   size_t ge_cap = 0;
   hipEvent_t ge_ev[2] = {nullptr, nullptr};

@@ -457,7 +457,10 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       return AIY_OK;
     case AIY_OPT_HIST_KRYLOV: h->hist_krylov = value != 0; return AIY_OK;
     case AIY_OPT_GE_RESIDENT: h->ge_resident = value != 0; return AIY_OK;
-    case AIY_OPT_GE_LOGSEC: h->ge_logsec = value != 0; return AIY_OK;
+    case AIY_OPT_GE_LOGSEC:
+      if (value < 0 || value > 2) return fail(h, AIY_ERR_ARG, "AIY_OPT_GE_LOGSEC must be 0, 1 or 2");
+      h->ge_logsec = (int)value;
+      return AIY_OK;
     case AIY_OPT_GE_EXTRAP_PERIOD:
       if (value < 4 || value > 1024) return fail(h, AIY_ERR_ARG, "AIY_OPT_GE_EXTRAP_PERIOD must be in [4, 1024]");
       h->ge_extrap_period = (int)value;

@@ -354,11 +354,13 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     the freed compute units (larger clusters); 0: one launch */
 #define AIY_OPT_GE_EXTRAP_PERIOD 13 /* device-resident GE search: EGM cycles between the geometric
                                     extrapolation checks (4 .. 1024; default 32) */
-#define AIY_OPT_GE_LOGSEC 14      /* value != 0 (default): with loose bracketing, while only
-                                    K_s < K_d has been seen the next point is a secant of
-                                    log(K_s / K_d) against log(1/beta - 1 - r) (aimed 20 % past the
-                                    predicted root, the distance to 1/beta - 1 cut by 2 .. 16)
-                                    instead of a bisection step; 0: bisection */
+#define AIY_OPT_GE_LOGSEC 14      /* 1: with loose bracketing, while only K_s < K_d has been seen
+                                    the next point is a secant of log(K_s / K_d) against
+                                    log(1/beta - 1 - r) through the last two points (aimed 20 %
+                                    past the predicted root, the distance to 1/beta - 1 cut by
+                                    2 .. 16) instead of a bisection step, and Brent runs in those
+                                    coordinates; 2 (default): also a unit-slope step from a single
+                                    point; 0: bisection bracketing, Brent in r */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */

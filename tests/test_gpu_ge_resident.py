@@ -94,3 +94,32 @@ def test_rebalancing_relaunches_match_one_launch(gpu):
     assert np.all(reb.status == 0) and np.all(one.status == 0)
     assert np.max(np.abs(reb.r - one.r)) <= 2e-7
     assert np.max(np.abs(reb.KtoY - one.KtoY) / one.KtoY) <= 2e-6
+
+
+def test_logsec_levels_same_roots(gpu):
+    """AIY_OPT_GE_LOGSEC 0 / 1 / 2 (bisection bracketing and Brent in r; the two-point
+    log-secant bracketing and Brent in log coordinates; also the one-point step): the same
+    roots to the search tolerance on both the resident search and the host-driven loop, and
+    the log-coordinate levels take fewer evaluations than bisection bracketing on the resident
+    search (whose bisection_steps count each calibration's own evaluations)."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    h = _lib.handle(gpu.index)
+    cals = table2_calibrations()
+    with pytest.raises(RuntimeError):
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOGSEC, 3), "opt")
+    out = {}
+    try:
+        for lvl in (0, 1, 2):
+            h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOGSEC, lvl), "opt")
+            for resident in (True, False):
+                out[lvl, resident] = solve_table2(cals, n_a=2000, device=gpu, method="brent", resident=resident)
+    finally:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOGSEC, 2), "opt")
+    base = out[0, False]
+    for (lvl, resident), res in out.items():
+        print(f"\nlogsec {lvl} resident {resident}: evaluations {int(np.sum(res.bisection_steps))}, "
+              f"max |dr| {np.max(np.abs(res.r - base.r)):.2e}")
+        assert np.all(res.status == 0)
+        assert np.max(np.abs(res.r - base.r)) <= 2e-7
+    assert np.sum(out[2, True].bisection_steps) < np.sum(out[0, True].bisection_steps)

@@ -37,6 +37,8 @@ for step in "$@"; do
     ls0) run ls0 300 python -u tools/ge_resident_profile.py --modes resident,host --reps 3 --logsec 0 ;;
     g24h) run g24h 300 python -u tools/ge_resident_profile.py --modes resident,host --reps 3 ;;
     g24off) run g24off 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --rebalance 0 ;;
+    stress_ls) run stress_ls 400 python -u tools/stress_logsec.py ;;
+    lsl) run lsl 400 $PYT -s tests/test_gpu_ge_resident.py -k logsec_levels ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
