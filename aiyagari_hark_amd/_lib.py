@@ -127,6 +127,7 @@ SIGNATURES = {
                                                vp, vp, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                vp, vp, vp, vp]),
     "aiy_set_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int64]),
+    "aiy_get_option": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "aiy_index_ints_per_row": (ctypes.c_int32, []),
     "aiy_panel_table_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "aiy_panel_build": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -145,6 +146,7 @@ SIGNATURES = {
     "aiy_ge_resident_plan": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_int32_p]),
     "aiy_ge_last_profile": (ctypes.c_int32, [vp, c_double_p, ctypes.c_int32]),
     "aiy_ge_last_eval_log": (ctypes.c_int32, [vp, c_double_p, ctypes.c_int32]),
+    "aiy_ge_last_rounds": (ctypes.c_int32, [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "aiy_ge_launch_stats": (ctypes.c_int32, [vp, c_double_p, ctypes.POINTER(ctypes.c_int64), c_double_p, c_double_p,
                                              ctypes.c_int32]),
     "aiy_ge_stationary_work_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
@@ -204,6 +206,18 @@ class Handle:
         if rc != AIY_OK:
             msg = self.lib.aiy_last_error(self.h)
             raise AiyagariLibError(f"{what} failed: {ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int64()
+        self.check(self.lib.aiy_get_option(self.h, int(option), ctypes.byref(v)), "aiy_get_option")
+        return int(v.value)
+
+    def set_options(self, values: dict) -> dict:
+        """Set several options; returns their previous values (pass them back to restore)."""
+        prev = {k: self.get_option(k) for k in values}
+        for k, v in values.items():
+            self.check(self.lib.aiy_set_option(self.h, int(k), int(v)), "aiy_set_option")
+        return prev
 
     def close(self):
         if getattr(self, "h", None):

@@ -745,6 +745,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       if (tid == 0) {
         st.its_sum += -mv - 2;
         st.in_hist = 1;
+        if (w == 0) __hip_atomic_fetch_add(to_global(g.done_ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       stopped = true;
@@ -839,11 +840,14 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
   const int g_min = (n_a + 2 * 512 - 1) / (2 * 512);
+  // the cluster reductions (ge_reduce, hist_bicg.h) read at most kHcMaxG workgroups
+  if (g_min > kHcMaxG || g_min > cus) return false;
   const int g_cap = h->hist_cluster_cap > 0 ? h->hist_cluster_cap : 32;
   int G = std::max(g_min, std::min(std::min(g_cap, kHcMaxG), cus / n_cal));
   G = std::min(G, n_a);
   p.nj = (n_a + G - 1) / G;
   p.G = (n_a + p.nj - 1) / p.nj;
+  if (p.G > kHcMaxG) return false;
   if (p.nj > kGeMaxTiles * kTile) return false;
   if ((long long)p.G * n_cal > cus) return false;
   p.th = 512;
@@ -982,6 +986,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   std::vector<int> active(n_cal), done(n_cal, 0), resume(n_cal, 0);
   for (int c = 0; c < n_cal; ++c) active[c] = c;
   h->ge_rounds = 0;
+  h->ge_mid_stops = 0;
   while (!active.empty()) {
     const int n = (int)active.size();
     GePlan p;
@@ -1010,8 +1015,8 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
     AIY_HIP(h, hipEventRecord(h->ge_ev[0], st));
     AIY_HIP(h, hipLaunchKernel(p.fn, dim3(p.blocks), dim3(p.th), args, p.lds, st));
     AIY_HIP(h, hipEventRecord(h->ge_ev[1], st));
-    unsigned err = 0;
-    AIY_HIP(h, hipMemcpyAsync(&err, g.err, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    unsigned errw[3] = {0, 0, 0};   // error, finished clusters, clusters stopped inside a solve
+    AIY_HIP(h, hipMemcpyAsync(errw, g.err, sizeof(errw), hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipMemcpyAsync(done.data(), g.out_done, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipStreamSynchronize(st));
     float ms = 0.f;
@@ -1020,6 +1025,8 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
       h->ge_launches += 1;
     }
     ++h->ge_rounds;
+    h->ge_mid_stops += errw[2];
+    const unsigned err = errw[0];
     if (err == 1u)
       return fail(h, AIY_ERR_STATE, "device-resident GE: cluster barrier timed out (workgroups not co-resident?)");
     if (err) return fail(h, AIY_ERR_STATE, "device-resident GE: histogram shape does not fit (error %u)", err);
@@ -1080,6 +1087,15 @@ extern "C" int32_t aiy_ge_resident_plan(aiy_handle* h, int32_t n_cal, int32_t S,
   out4[2] = p.kc;
   out4[3] = p.blocks;
   return 1;
+}
+
+// Launches of the last device-resident search (1 + rebalancing relaunches) and how many of
+// its cluster stops happened inside a distribution solve (resumed from the iterate).
+extern "C" int32_t aiy_ge_last_rounds(aiy_handle* h, int32_t* launches, int32_t* mid_solve_stops) {
+  if (!h) return AIY_ERR_ARG;
+  if (launches) *launches = h->ge_rounds;
+  if (mid_solve_stops) *mid_solve_stops = h->ge_mid_stops;
+  return AIY_OK;
 }
 
 extern "C" int32_t aiy_ge_launch_stats(aiy_handle* h, double* ms_sum, int64_t* launches, double* point_matvecs,

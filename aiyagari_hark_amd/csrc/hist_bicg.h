@@ -574,8 +574,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) Vl[vidx(k, s)] = rv[k][s];
     // rebalancing stop request: polled every 8th iteration by thread 0 into LDS (the matvec's
-    // barriers make it visible; the partial below carries it to every workgroup)
-    if (r.stop_ctr != nullptr && tid == 0 && (mv & 15) == 0)
+    // barriers make it visible; the partial below carries it to every workgroup).  mv grows by
+    // 2 per iteration and is odd after a restart's true-residual matvec, so the iteration
+    // number is mv >> 1
+    if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
       s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
     if (!matvec(pv, tv)) return -1;
     ++mv;

@@ -480,3 +480,26 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
     default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
   }
 }
+
+// Current value of a handle option (the values aiy_set_option takes), so callers can save
+// and restore what they change.
+extern "C" int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value) {
+  if (!h || !value) return AIY_ERR_ARG;
+  switch (option) {
+    case AIY_OPT_USE_GRAPHS: *value = h->use_graphs; return AIY_OK;
+    case AIY_OPT_RESIDENT: *value = h->use_resident; return AIY_OK;
+    case AIY_OPT_RESIDENT_SHAPE: *value = h->res_shape; return AIY_OK;
+    case AIY_OPT_HIST_FUSED: *value = h->hist_fused; return AIY_OK;
+    case AIY_OPT_RESIDENT_STREAM: *value = h->res_stream; return AIY_OK;
+    case AIY_OPT_HIST_RESIDENT: *value = h->hist_resident; return AIY_OK;
+    case AIY_OPT_HIST_ACCEL: *value = h->hist_accel; return AIY_OK;
+    case AIY_OPT_HIST_KRYLOV: *value = h->hist_krylov; return AIY_OK;
+    case AIY_OPT_GE_RESIDENT: *value = h->ge_resident; return AIY_OK;
+    case AIY_OPT_GE_LOGSEC: *value = h->ge_logsec; return AIY_OK;
+    case AIY_OPT_GE_EXTRAP_PERIOD: *value = h->ge_extrap_period; return AIY_OK;
+    case AIY_OPT_GE_REBALANCE: *value = h->ge_rebalance; return AIY_OK;
+    case AIY_OPT_CU_LIMIT: *value = h->cu_limit; return AIY_OK;
+    case AIY_OPT_HIST_CLUSTER: *value = h->hist_cluster_cap; return AIY_OK;
+    default: return fail(h, AIY_ERR_ARG, "unknown option %d", option);
+  }
+}

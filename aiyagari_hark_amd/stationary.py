@@ -261,12 +261,12 @@ def resident_plan(device, n_cal, S, n_a, cu_share=1.0):
     aiy_ge_stationary would run the host-driven loop instead."""
     dev = _resolve_device(device)
     h = _lib.handle(dev.index)
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 1), "aiy_set_option")
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, _cu_limit(dev, cu_share)), "aiy_set_option")
+    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT: 1, _lib.AIY_OPT_CU_LIMIT: _cu_limit(dev, cu_share)})
     out = (ctypes.c_int32 * 4)()
-    ok = h.lib.aiy_ge_resident_plan(h.h, int(n_cal), int(S), int(n_a), out)
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 0), "aiy_set_option")
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, 0), "aiy_set_option")
+    try:
+        ok = h.lib.aiy_ge_resident_plan(h.h, int(n_cal), int(S), int(n_a), out)
+    finally:
+        h.set_options(prev)
     return tuple(out) if ok == 1 else None
 
 
@@ -303,21 +303,21 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
     opt.status_out = ctypes.addressof(status)
     r, K, Ks = (ctypes.c_double * n)(), (ctypes.c_double * n)(), (ctypes.c_double * n)()
     steps, cyc, its = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, int(bool(resident))), "aiy_set_option")
-    h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, _cu_limit(b.device, cu_share)), "aiy_set_option")
+    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT: int(bool(resident)),
+                          _lib.AIY_OPT_CU_LIMIT: _cu_limit(b.device, cu_share)})
     try:
         h.check(h.lib.aiy_ge_stationary(h.h, ctypes.byref(model), ctypes.byref(opt), _lib.ptr(work), r, K, Ks,
                                         ctypes.byref(steps), ctypes.byref(cyc), ctypes.byref(its),
                                         _lib.stream_ptr(stream)),
                 "aiy_ge_stationary")
     finally:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_RESIDENT, 0), "aiy_set_option")
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_CU_LIMIT, 0), "aiy_set_option")
+        h.set_options(prev)
     return (np.array(r[:]), np.array(K[:]), np.array(Ks[:]), int(steps.value), int(cyc.value), int(its.value),
             np.array(status[:], dtype=np.int32))
 
 
 _GROUP_CTX = {}   # (device, group) -> (library handle, torch stream), reused across sweeps
+_GROUP_CARRY_OPTIONS = (_lib.AIY_OPT_GE_LOGSEC, _lib.AIY_OPT_GE_REBALANCE, _lib.AIY_OPT_GE_EXTRAP_PERIOD)
 
 
 def _close_groups():
@@ -355,13 +355,16 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
     cus = _device_cus(dev, cu_share)
     cap = max(1, min(32, cus // n))
     cur = torch.cuda.current_stream(dev)
+    # the search options a caller set on the device's shared handle carry over to the groups
+    shared = _lib.handle(dev.index)
+    carry = {o: shared.get_option(o) for o in _GROUP_CARRY_OPTIONS}
     jobs = []
     for gi, ii in enumerate(idx):
         key = (dev.index, gi)
         if key not in _GROUP_CTX:
             _GROUP_CTX[key] = (_lib.Handle(dev.index), torch.cuda.Stream(dev))
         h, st = _GROUP_CTX[key]
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, cap), "aiy_set_option")
+        h.set_options(dict(carry, **{_lib.AIY_OPT_HIST_CLUSTER: cap}))
         b = StationaryBatch([cals[i] for i in ii], aGrid, device=dev)
         sub = lambda x: None if x is None else np.broadcast_to(np.asarray(x, float), (n,))[ii]  # noqa: E731
         st.wait_stream(cur)

@@ -341,11 +341,13 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     BiCGSTAB from the given mass (hist_krylov.hip; stops at a mass
                                     T x with max|T x - x| < tol, the plain iteration's rule; counts
                                     are matvecs); takes precedence over AIY_OPT_HIST_ACCEL */
-#define AIY_OPT_GE_RESIDENT 10    /* value != 0 (default): aiy_ge_stationary runs the whole search of
+#define AIY_OPT_GE_RESIDENT 10    /* value != 0: aiy_ge_stationary runs the whole search of
                                     every calibration in ONE device-resident launch (each
                                     calibration's cluster: EGM cycles, lottery, BiCGSTAB, K_s and the
                                     root search on device, ge_resident.hip) when accel < 0, S <= 8
-                                    and every cluster fits the device at once; else the host loop */
+                                    and every cluster fits the device at once; else the host loop.
+                                    A new handle starts at 0 (the host loop); the Python wrapper
+                                    (stationary.solve_table2) sets it by default */
 #define AIY_OPT_CU_LIMIT 11       /* compute units the resident launches of this handle may fill
                                     (0: the device's; several processes sharing one GPU: a share) */
 #define AIY_OPT_GE_REBALANCE 12   /* value q in [1, 100] (default 50): the device-resident GE search
@@ -362,6 +364,8 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     coordinates; 2 (default): also a unit-slope step from a single
                                     point; 0: bisection bracketing, Brent in r */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
+/* The current value of an option (so a caller can save and restore what it changes). */
+int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);
 
 /* -------------------------- RCCL binding (multi-GPU, §8e) -------------------------- */
 /* 128-byte ncclUniqueId created by rank 0 and broadcast by the host. */
@@ -472,6 +476,11 @@ int32_t aiy_ge_last_profile(aiy_handle* h, double* out, int32_t n_cal);
 /* Per-evaluation log of the last device-resident search: out[(c * 32 + e) * 6 + k], k = r,
    (K_s - K_d) / K_d, EGM cycles, matvecs, loose flag, microseconds (measurement hook). */
 int32_t aiy_ge_last_eval_log(aiy_handle* h, double* out, int32_t n_cal);
+
+/* Launches of the last device-resident search (1 + its rebalancing relaunches) and how many
+ * cluster stops happened inside a distribution solve (that solve resumes from its iterate in
+ * the next launch).  Host-only. */
+int32_t aiy_ge_last_rounds(aiy_handle* h, int32_t* launches, int32_t* mid_solve_stops);
 
 /* Resident-histogram launch statistics (measurement hook): kernel milliseconds summed over
  * the device-resident distribution-iteration launches since the last reset (HIP events on

@@ -34,6 +34,10 @@ def test_resident_plan_shapes(gpu):
     half = resident_plan(gpu, 24, 7, 10_000, cu_share=0.5)
     assert half is None or half[0] * 24 <= 128
     assert resident_plan(gpu, 3, 25, 50_000) is None     # stress shape: the host loop
+    # clusters above 128 workgroups would escape the cluster reductions: the host loop runs
+    assert resident_plan(gpu, 1, 7, 150_000) is None
+    p1 = resident_plan(gpu, 1, 7, 120_000)
+    assert p1 is None or p1[0] <= 128
 
 
 @pytest.mark.parametrize("method", ["bisect", "brent"])
@@ -78,6 +82,8 @@ def test_rebalancing_relaunches_match_one_launch(gpu):
     """AIY_OPT_GE_REBALANCE: clusters stop at evaluation boundaries once half the launch's
     calibrations have finished and the rest continue from their saved search state on larger
     clusters; the roots agree with the single launch to the search tolerance."""
+    import ctypes
+
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
     h = _lib.handle(gpu.index)
@@ -88,9 +94,14 @@ def test_rebalancing_relaunches_match_one_launch(gpu):
         one = solve_table2(cals, **kw)
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, 50), "opt")
         reb = solve_table2(cals, **kw)
+        launches, mid = ctypes.c_int32(), ctypes.c_int32()
+        h.check(h.lib.aiy_ge_last_rounds(h.h, ctypes.byref(launches), ctypes.byref(mid)), "rounds")
     finally:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, 50), "opt")
-    print(f"\nsteps one {one.bisection_steps} rebalanced {reb.bisection_steps}; max |dr| {np.max(np.abs(reb.r - one.r)):.2e}")
+    print(f"\nsteps one {one.bisection_steps} rebalanced {reb.bisection_steps}; max |dr| {np.max(np.abs(reb.r - one.r)):.2e}; "
+          f"{launches.value} launches, {mid.value} stops inside a distribution solve")
+    # relaunches happened, and some clusters stopped inside a BiCGSTAB solve (resumed from x)
+    assert launches.value >= 2 and mid.value >= 1
     assert np.all(reb.status == 0) and np.all(one.status == 0)
     assert np.max(np.abs(reb.r - one.r)) <= 2e-7
     assert np.max(np.abs(reb.KtoY - one.KtoY) / one.KtoY) <= 2e-6

@@ -40,6 +40,8 @@ for step in "$@"; do
     stress_ls) run stress_ls 400 python -u tools/stress_logsec.py ;;
     lsl) run lsl 400 $PYT -s tests/test_gpu_ge_resident.py -k logsec_levels ;;
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
+    panelvar3) run panelvar3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,0,1,200]]' AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,noindex=aiyagari_hark_amd/lib/variants/libaiyagari_noindex.so,norecord=aiyagari_hark_amd/lib/variants/libaiyagari_norecord.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
+    panelvar1) run panelvar1 400 env NAG=1000006 T=400 OPTS='[[1,0,0,0,400],[1,0,0,1,400]]' AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,noindex=aiyagari_hark_amd/lib/variants/libaiyagari_noindex.so,norecord=aiyagari_hark_amd/lib/variants/libaiyagari_norecord.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
