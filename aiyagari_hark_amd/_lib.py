@@ -135,6 +135,7 @@ SIGNATURES = {
     "aiy_build_index": (ctypes.c_int32, [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]),
     "aiy_comm_unique_id": (ctypes.c_int32, [vp]),
     "aiy_comm_init": (ctypes.c_int32, [vp, vp, ctypes.c_int32, ctypes.c_int32]),
+    "aiy_comm_bind": (ctypes.c_int32, [vp, vp]),
     "aiy_comm_destroy": (ctypes.c_int32, [vp]),
     "aiy_allreduce_sum": (ctypes.c_int32, [vp, vp, ctypes.c_int64, vp]),
     "aiy_hist_lottery": (ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp,

@@ -26,7 +26,7 @@ extern "C" int32_t aiy_create(int32_t device, aiy_handle** out) {
 extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (!h) return AIY_OK;
   (void)hipSetDevice(h->device);
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   if (h->d_dist) (void)hipFree(h->d_dist);
   if (h->d_last) (void)hipFree(h->d_last);
   if (h->d_egm_hint) (void)hipFree(h->d_egm_hint);
@@ -84,13 +84,37 @@ extern "C" int32_t aiy_comm_init(aiy_handle* h, const void* unique_id128, int32_
   }
   h->nranks = nranks;
   h->rank = rank;
+  h->comm_owned = true;
+  return AIY_OK;
+}
+
+// Borrow a communicator the caller owns (e.g. torch.distributed's RCCL process group, whose
+// ncclComm_t ProcessGroupNCCL._comm_ptr() returns): the library enqueues its all-reduces on
+// it and never destroys it, so a process keeps ONE communicator per device.  The caller keeps
+// it alive until aiy_comm_destroy (which only unbinds it) or aiy_destroy.
+extern "C" int32_t aiy_comm_bind(aiy_handle* h, void* comm) {
+  if (!h) return AIY_ERR_ARG;
+  if (!comm) return aiy::fail(h, AIY_ERR_ARG, "null communicator");
+  if (h->comm) return aiy::fail(h, AIY_ERR_STATE, "communicator already bound");
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int nranks = 0, rank = 0, dev = -1;
+  ncclResult_t r = ncclCommCount(c, &nranks);
+  if (r == ncclSuccess) r = ncclCommUserRank(c, &rank);
+  if (r == ncclSuccess) r = ncclCommCuDevice(c, &dev);
+  if (r != ncclSuccess) return aiy::fail(h, AIY_ERR_COMM, "communicator query: %s", ncclGetErrorString(r));
+  if (dev != h->device) return aiy::fail(h, AIY_ERR_ARG, "communicator is on device %d, handle on %d", dev, h->device);
+  h->comm = c;
+  h->comm_owned = false;
+  h->nranks = nranks;
+  h->rank = rank;
   return AIY_OK;
 }
 
 extern "C" int32_t aiy_comm_destroy(aiy_handle* h) {
   if (!h) return AIY_ERR_ARG;
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   h->comm = nullptr;
+  h->comm_owned = false;
   h->nranks = 1;
   h->rank = 0;
   return AIY_OK;

@@ -90,6 +90,7 @@ struct aiy_handle {
   bool res_stream = false;           // AIY_OPT_RESIDENT_STREAM
   // RCCL
   ncclComm_t comm = nullptr;
+  bool comm_owned = false;           // created by aiy_comm_init (destroyed with the handle)
   int nranks = 1, rank = 0;
   // stream hand-off between calls that share the scratch above (aiy::use_stream)
   hipStream_t last_stream = nullptr;

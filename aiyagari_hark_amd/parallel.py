@@ -47,12 +47,39 @@ def initial_labor_states(n_total: int, n_lab: int, offset: int, n_local: int):
     return (np.arange(offset, offset + n_local) // per).astype(np.uint8)
 
 
-def bind_rccl(handle: "_lib.Handle", group=None):
-    """Create an RCCL communicator over the ranks of ``group`` and bind it to the
-    libaiyagari handle (rank 0 makes the ncclUniqueId, torch.distributed broadcasts it)."""
+def torch_comm_ptr(group=None, device=None):
+    """The ncclComm_t of torch.distributed's RCCL process group on ``device`` (an int), or
+    None when the backend is not nccl or the communicator is not created yet.  torch's
+    bundled librccl is the only RCCL in the process (libaiyagari's DT_NEEDED librccl.so.1
+    resolves to the already-loaded copy), so the pointer is valid for the library."""
+    import torch
+    import torch.distributed as dist
+    try:
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        if dist.get_backend(pg) != "nccl":
+            return None
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        ptr = int(pg._get_backend(dev)._comm_ptr())
+        return ptr or None
+    except (AttributeError, RuntimeError, ValueError):
+        return None
+
+
+def bind_rccl(handle: "_lib.Handle", group=None, prefer_torch=True):
+    """Bind an RCCL communicator over the ranks of ``group`` to the libaiyagari handle.
+
+    prefer_torch: borrow torch.distributed's own communicator (aiy_comm_bind), so the
+    process holds ONE communicator per device and the library's per-period all-reduces and
+    torch's collectives are ordered on one comm; else (or when torch's is not available)
+    create the library's own (rank 0 makes the ncclUniqueId, torch.distributed broadcasts it).
+    Returns (world, rank, "torch" | "own")."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    if prefer_torch:
+        ptr = torch_comm_ptr(group)
+        if ptr is not None and handle.lib.aiy_comm_bind(handle.h, ctypes.c_void_p(ptr)) == _lib.AIY_OK:
+            return world, rank, "torch"
     buf = ctypes.create_string_buffer(128)
     if rank == 0:
         rc = handle.lib.aiy_comm_unique_id(buf)
@@ -64,7 +91,7 @@ def bind_rccl(handle: "_lib.Handle", group=None):
     dist.broadcast_object_list(obj, src=src, group=group)
     uid = ctypes.create_string_buffer(obj[0], 128)
     handle.check(handle.lib.aiy_comm_init(handle.h, uid, world, rank), "aiy_comm_init")
-    return world, rank
+    return world, rank, "own"
 
 
 def unbind_rccl(handle: "_lib.Handle"):

@@ -212,13 +212,18 @@ def table2_leg(args, world, rank, dev):
         # (N_a + 1) per calibration and EGM cycle
         kern = "ge_cluster_kernel (device-resident GE search: EGM cycles + lottery + BiCGSTAB + root search)"
         hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * ge_pts + EGM_BYTES_PER_NODE_CYCLE * 7 * (args.grid + 1) * ge_cyc
+        # the same launches in SURVEY.md §8d's own units: 28 B per point-iteration of the
+        # histogram (no iterate updates counted) + 32 B per (state, node) per EGM cycle
+        s8d_bytes = HIST_BYTES_PER_POINT * ge_pts + EGM_BYTES_PER_NODE_CYCLE * 7 * (args.grid + 1) * ge_cyc
         hist_ms, hist_n = ge_ms, ge_n
     else:
         # dominant kernel: the device-resident BiCGSTAB distribution solve (one launch per
         # K_s(r) evaluation); algorithmic bytes 52 per (state, node) point per matvec
         kern = "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery stationary distribution)"
         hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
+        s8d_bytes = HIST_BYTES_PER_POINT * point_iters
     hist_gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
+    s8d_gbs = s8d_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[float(x) for x in res.r], KtoY=[float(x) for x in res.KtoY],
                                    evaluations=res.bisection_steps), world)
     r = [None] * len(cells)
@@ -229,7 +234,8 @@ def table2_leg(args, world, rank, dev):
     out = dict(seconds_per_sweep=el / args.steps, value=len(cells) * args.steps / el, kernel=kern,
                resident=ge_n > 0, egm_cycles_per_sweep=ge_cyc / args.steps if ge_n else None,
                hist_kernel_ms_per_sweep=hist_ms / args.steps, hist_launches_per_sweep=hist_n / args.steps,
-               hist_gbs=hist_gbs, hist_bytes_per_launch=hist_bytes / max(1, hist_n),
+               hist_gbs=hist_gbs, hist_bytes_per_launch=hist_bytes / max(1, hist_n), s8d_gbs=s8d_gbs,
+               s8d_bytes_per_launch=s8d_bytes / max(1, hist_n),
                hist_avg_launch_ms=hist_ms / max(1, hist_n),
                evaluations_rank0=per_rank[0]["evaluations"], r_percent=[round(100 * x, 6) for x in r],
                saving_rate_percent=[round(100 * 0.08 * x, 5) for x in kty])
@@ -420,8 +426,11 @@ def configs3_leg(args, world, rank, dev):
     # rehearsal, the two-step period with the caller's all-reduce
     gloo = world > 1 and dist.get_backend() == "gloo"
     allreduce = torch_allreduce() if gloo else None
+    comm = None
     if world > 1 and not gloo:
-        bind_rccl(h)
+        # torch's own RCCL communicator when it exposes one (one communicator per device),
+        # else the library's
+        comm = bind_rccl(h)[2]
     try:
         p, reset = c3_panel(dev, econ, agent, n_total, T, world, rank)
         p.run(0, 64, shock_mode="philox", seed=C3_SEED, ge_iter=0, allreduce=allreduce)   # warm-up
@@ -459,6 +468,7 @@ def configs3_leg(args, world, rank, dev):
                          "frac": gbs / HBM_PEAK_GBS,
                          "traffic": pmc_traffic_periods("sim_resident_kernel_stream", T) if world == 1 else None,
                          "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": kern_ms},
+               communicator=comm,
                workload=f"BASELINE configs[3]: {n_total} agents x {T} periods, agents sharded over {world} rank(s), "
                         "Philox by global agent index, per-period all-reduce of the asset sum when sharded "
                         f"({'gloo two-step rehearsal' if gloo else 'RCCL'})")
@@ -683,6 +693,12 @@ def cpu_baseline(n_a, r_gpu, budget_workers=16, ks_ge_iterations=None):
                                      f"once: {all_wall:.1f} s wall (per solve {min(x[0] for x in res):.1f}-"
                                      f"{max(x[0] for x in res):.1f} s); {workers} = the GPU box's CPU share per GPU "
                                      f"(nproc {n_cpu})")},
+            # the whole node: the measured per-process rate x nproc, an extrapolation (the box
+            # limits a command to its per-GPU CPU share, so 256 processes are not run here)
+            "all_cores_node_estimate": {"value": (workers / all_wall) * n_cpu / workers, "unit": "GE solves/s",
+                                        "cores": n_cpu, "kind": "port", "measured": False,
+                                        "sample": (f"all_cores' {workers}-process rate scaled to nproc = {n_cpu} "
+                                                   "(linear in processes: one solve per process, no shared state)")},
             "ks_reference": ks}
 
 
@@ -758,6 +774,12 @@ def main():
                                 "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
                                 "updates)"),
                      "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"]),
+                     # the same kernel time in SURVEY.md §8d's units (28 B per histogram point-iteration,
+                     # 32 B per EGM node-cycle; the 24 B of BiCGSTAB iterate updates not counted)
+                     "s8d_units": {"achieved": t2["s8d_gbs"], "frac": t2["s8d_gbs"] / HBM_PEAK_GBS,
+                                   "algorithmic_bytes_per_launch": t2["s8d_bytes_per_launch"],
+                                   "note": "28 B per state x node point per matvec + 32 B per state x node per EGM "
+                                           "cycle (SURVEY.md §8d)"},
                      # concurrent launches (independent groups) overlap: the device-level rate is the
                      # algorithmic bytes of a whole sweep over the sweep's wall time
                      "device_aggregate": {"achieved": sweep_bytes / t2["seconds_per_sweep"] / 1e9,

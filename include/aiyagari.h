@@ -371,6 +371,11 @@ int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);
 /* 128-byte ncclUniqueId created by rank 0 and broadcast by the host. */
 int32_t aiy_comm_unique_id(void* out128);
 int32_t aiy_comm_init(aiy_handle* h, const void* unique_id128, int32_t nranks, int32_t rank);
+/* Bind a communicator the caller owns (an ncclComm_t, e.g. torch.distributed's RCCL group:
+ * ProcessGroupNCCL._comm_ptr()) instead of creating one: one communicator per device in the
+ * process.  It must be on the handle's device; aiy_comm_destroy then only unbinds it. */
+int32_t aiy_comm_bind(aiy_handle* h, void* comm);
+/* Unbind the communicator (destroying it when aiy_comm_init created it). */
 int32_t aiy_comm_destroy(aiy_handle* h);
 /* Sum-all-reduce of n doubles in place over the bound communicator (asynchronous). */
 int32_t aiy_allreduce_sum(aiy_handle* h, double* buf, int64_t n, aiy_stream stream);

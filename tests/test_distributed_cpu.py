@@ -83,6 +83,8 @@ def _worker(rank, world, port, out_q, n_total, T, seed):
             return float(t.item())
 
         hist, a, lab = _panel_history(a0, lab0, off, T, seed, fx, allreduce, n_total)
+        # gloo has no RCCL communicator to lend the library: bind_rccl creates its own there
+        assert par.torch_comm_ptr() is None
         out_q.put((rank, hist, a, lab))
     finally:
         dist.destroy_process_group()

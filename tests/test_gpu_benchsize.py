@@ -236,3 +236,25 @@ def test_bench_two_rank_rehearsal_matches_one_rank(gpu):
     k1, k2 = np.array(one["configs3"]["K_first"]), np.array(two["configs3"]["K_first"])
     assert np.max(np.abs(k1 - k2) / k1) < 1e-12
     assert abs(one["configs3"]["K_final"] - two["configs3"]["K_final"]) / one["configs3"]["K_final"] < 1e-12
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_rank_rehearsal_matches_one_rank(gpu):
+    """The driver's 8-GPU run rehearsed on one GPU: bench.py --gpus 8 --dist-backend gloo
+    starts 8 rank processes on device 0 (each with 1/8 of the compute units for its
+    resident clusters): 3 Table II cells per rank, configs[3] agents in 8 shards with the
+    per-period sum through the two-step period.  n_gpus is 8, every cell's r equals the
+    one-rank r, and the K history matches to 1e-12."""
+    one = _bench_line([], 180)
+    eight = _bench_line(["--gpus", "8", "--dist-backend", "gloo"], 480)
+    assert eight["n_gpus"] == 8 and "rehearsal" in eight
+    assert all(x is not None for x in eight["table2"]["r_percent"])
+    # 3 cells per rank run in one launch, the single rank's 24 with rebalancing relaunches on
+    # larger clusters (another summation order of K_s): equal within the search tolerance
+    # (r_tol = 1e-7, i.e. 1e-5 percentage points)
+    dr = np.max(np.abs(np.array(eight["table2"]["r_percent"]) - one["table2"]["r_percent"]))
+    print(f"\n8-rank rehearsal: max |dr| = {dr:.2e} pp")
+    assert dr <= 1e-5
+    k1, k8 = np.array(one["configs3"]["K_first"]), np.array(eight["configs3"]["K_first"])
+    assert np.max(np.abs(k1 - k8) / k1) < 1e-12
+    assert abs(one["configs3"]["K_final"] - eight["configs3"]["K_final"]) / one["configs3"]["K_final"] < 1e-12

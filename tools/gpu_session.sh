@@ -42,6 +42,10 @@ for step in "$@"; do
     g24) run g24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 ;;
     panelvar3) run panelvar3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,0,1,200]]' AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,noindex=aiyagari_hark_amd/lib/variants/libaiyagari_noindex.so,norecord=aiyagari_hark_amd/lib/variants/libaiyagari_norecord.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panelvar1) run panelvar1 400 env NAG=1000006 T=400 OPTS='[[1,0,0,0,400],[1,0,0,1,400]]' AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,noindex=aiyagari_hark_amd/lib/variants/libaiyagari_noindex.so,norecord=aiyagari_hark_amd/lib/variants/libaiyagari_norecord.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
+    hphase_stress) run hphase_stress 300 env STRESS=1 AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/hist_phases.py 3 0 -1 ;;
+    hphase_t2) run hphase_t2 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/hist_phases.py 24 0 -1 ;;
+    trace_c4) export TMPDIR=/tmp; run trace_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c4 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --legs configs4 ;;
+    trace_c3) export TMPDIR=/tmp; run trace_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c3 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs3 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
