@@ -30,7 +30,9 @@ struct HcRun {
   int* span;              // [launch cals][G][SMAX][4] (first, len, left base, right base)
   unsigned* ctr;          // [launch cals][kHcCtrStride]
   double* dist;           // [launch cals][2][G][4]: sup-norm change, Aitken dot products, valid
-  double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0)
+  double* dbuf;           // [n_cal][S][n_a] stored differences for the Aitken step (accel > 0);
+                          // pull form (hist_pull.h): [n_cal][4][S][n_a] BiCGSTAB vectors r, p, v, t
+  int* ainv;              // pull form: [n_cal][S][n_a + 1] inverse lottery
   int accel;              // Aitken extrapolation period E (0: plain iteration = the oracle's)
   int* iters_out;         // [n_cal]
   unsigned* err;          // 0 ok, 1 timeout, 2 span overflow / not monotone, 3 candidate overflow
@@ -137,5 +139,9 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
 // BiCGSTAB form of the cluster kernel (hist_krylov.hip) for (S, padded S, columns per
 // thread) and its state count (*smax_k); nullptr when there is no instantiation
 const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k);
+// pull form (hist_pull.h) for S > 8: the kernel, and its dynamic LDS for n_own columns
+const void* hist_pull_pick(int S);
+size_t hist_pull_lds(int S, int n_own);
+constexpr int kHpTH = 512;
 
 }  // namespace aiy

@@ -36,6 +36,7 @@
 #include "internal.h"
 #include "hist_cluster.h"
 #include "hist_bicg.h"
+#include "hist_pull.h"
 
 namespace aiy {
 
@@ -82,6 +83,57 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
 }
+
+// The pull form for many income states (hist_pull.h): one solve per launch, vectors in HBM.
+template <int SMAX, int TH>
+__global__ __launch_bounds__(TH) void hist_pull_kernel(HcRun r) {
+  extern __shared__ int hp_dyn[];   // staged inverse lottery
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ int s_ex[2 * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  const HpShared<SMAX, TH> L{s_P, hp_dyn, s_ex, s_part, s_res, &s_flag, &s_stop};
+  const int G = r.G, S = r.S, n_a = r.n_a;
+  const int lc = blockIdx.x / G;
+  const int w = blockIdx.x - lc * G;
+  const int cal = r.cal0 + lc;
+  const size_t row0 = (size_t)cal * S;
+  const size_t pts = (size_t)S * n_a;
+  double* vec = r.dbuf + (size_t)cal * 4 * pts;
+  HpArgs a;
+  a.G = G; a.S = S; a.n_a = n_a; a.w = w;
+  a.j0 = w * r.nj;
+  a.j1 = min(a.j0 + r.nj, n_a);
+  a.LO = to_global(r.lo + row0 * n_a);
+  a.WL = to_global(r.wlo + row0 * n_a);
+  a.lottery_fresh = false;   // written by the lottery launch before this one
+  a.A = to_global(r.ainv + (size_t)cal * S * (n_a + 1));
+  a.X = to_global(r.mass + row0 * n_a);
+  a.R = to_global(vec);
+  a.P = to_global(vec + pts);
+  a.V = to_global(vec + 2 * pts);
+  a.T = to_global(vec + 3 * pts);
+  a.ctr = to_global(r.ctr + (size_t)lc * kHcCtrStride);
+  a.gran = to_global(reinterpret_cast<unsigned long long*>(r.dist) + (size_t)lc * 2 * G * kHcRedRec);
+  a.Pc = to_global(r.P + (size_t)cal * S * S);
+  a.tol = r.tolv ? r.tolv[cal] : r.tol;
+  a.max_iter = r.max_iter;
+  a.err = to_global(r.err);
+  a.stop_ctr = to_global((const unsigned*)nullptr);
+  a.stop_at = 0u;
+  unsigned nb = 0, ne = 0;
+  const int mv = hp_solve<SMAX, TH>(a, L, nb, ne);
+  if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
+}
+
+const void* hist_pull_pick(int S) {
+  // one instantiation: the register array of a column's S row sums is statically indexed
+  // (SMAX = 16 unrolled worse and spilled)
+  if (S <= 32) return reinterpret_cast<const void*>(hist_pull_kernel<32, kHpTH>);
+  return nullptr;
+}
+size_t hist_pull_lds(int S, int n_own) { return hp_lds_a_bytes<1>(n_own) * (size_t)S; }
 
 template <int SMAX, int KC, int TH>
 static const void* hk_fn() {

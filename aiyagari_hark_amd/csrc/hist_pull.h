@@ -1,0 +1,418 @@
+// Pull-form BiCGSTAB distribution solve of one calibration's cluster (build-defined row E2)
+// for many income states (configs[4]: 25-state Rouwenhorst at N_a = 50 000).
+//
+// The push form (hist_bicg.h) keeps r, p and the matvec result of every own point in
+// registers (3 S doubles per column) and scatters the lottery into LDS spans with atomics.
+// At S = 25 those registers do not fit (the kernel spilled ~1.1 KB per lane to scratch:
+// ~300 us per matvec) and the spans would need 25 rows of LDS.  Here the Krylov vectors live
+// in HBM ([S][n_a] rows per calibration, the calibration's 3 x 10 MB stay in the MALL) and a
+// matvec PULLS: a monotone lottery maps the sources of destination d of row s to contiguous
+// ranges, with A_s(d) = the first source j whose lottery index lo_j >= d,
+//
+//   T_s[d] = sum_{j in [A(d), A(d+1))} w_j q_j  +  sum_{j in [A(d-1), A(d))} (1 - w_j) q_j
+//
+// summed in ascending j: exactly np.add.at(T[s], lo, w q) followed by np.add.at(T[s],
+// lo + 1, (1 - w) q) of oracle/stationary.py hist_step -- no atomics, so every matvec is
+// deterministic run to run.  A destination with more than kHpHeavy sources (the borrowing
+// constraint, the top of the grid) is summed by its whole wave: lane-strided partials and a
+// fixed-order wave reduction.  Then mix: mass'[s'][d] = sum_s P[s, s'] T_s[d].
+//
+// Cross-workgroup data: only sources in an own column's "exported" prefix / suffix (whose
+// lo or lo + 1 falls outside the own columns) are read by other workgroups; they are stored
+// write-through (sc1) and drained before the cluster barrier, and foreign sources are read
+// with sc1 loads (MI355X_MICROARCH.md hand-off rules); everything else is plain.  The inverse
+// lottery A is built once per solve by a scatter over the own sources (sc1) and staged in LDS
+// for the own destinations.
+#pragma once
+
+#include "common.h"
+#include "hist_bicg.h"
+#include "hist_cluster.h"
+
+namespace aiy {
+
+constexpr int kHpHeavy = 64;   // sources of one destination above which its wave sums them
+
+struct HpArgs {
+  int G, S, n_a, w, j0, j1;
+  gptr<const int> LO;         // [S][n_a] lottery index
+  gptr<const double> WL;      // [S][n_a] lottery weight on lo
+  bool lottery_fresh;         // LO / WL written in this launch by other workgroups (sc1 loads)
+  gptr<int> A;                // [S][n_a + 1] inverse lottery (scratch)
+  gptr<double> X;             // [S][n_a] in: start, out: T x (own columns)
+  gptr<double> R, P, V, T;    // [S][n_a] BiCGSTAB vectors
+  gptr<unsigned> ctr;         // cluster barrier counter
+  gptr<unsigned long long> gran;   // [2][G][kHcRedRec] reduction granules
+  gptr<const double> Pc;      // [S][S]
+  double tol;
+  int max_iter;
+  gptr<unsigned> err;
+  gptr<const unsigned> stop_ctr;   // rebalancing stop (nullptr: never), as HkArgs
+  unsigned stop_at;
+};
+
+// LDS of the solve: P, the staged inverse lottery of the own destinations d in [j0 - 1, j1]
+// (row stride n_own + 2), the exported prefix / suffix bounds, reduction partials.
+template <int SMAX, int TH>
+struct HpShared {
+  double* s_P;                     // [SMAX][SMAX]
+  int* s_A;                        // [SMAX][span]
+  int* s_ex;                       // [SMAX][2]
+  double (*s_part)[TH / kWave];    // [kHkRed]
+  double* s_res;                   // [kHkRed]
+  int* s_flag;
+  int* s_stop;
+};
+template <int SMAX>
+__host__ __device__ constexpr size_t hp_lds_a_bytes(int n_own) {
+  return (size_t)SMAX * (size_t)(n_own + 2) * sizeof(int);
+}
+
+// Returns the matvecs of the solve, -1 when the cluster stops (error word: 1 timeout, 2 a
+// non-monotone lottery), or -(2 + matvecs) on a rebalancing stop (X holds the iterate).
+template <int SMAX, int TH>
+__device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH>& L, unsigned& nb, unsigned& ne) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const int G = r.G, S = r.S, n_a = r.n_a, w = r.w, j0 = r.j0, j1 = r.j1;
+  const int n_own = j1 - j0, span = n_own + 2;
+  const int* LO = (const int*)r.LO;
+  const double* WL = (const double*)r.WL;
+  int* A = (int*)r.A;
+  double* X = (double*)r.X;
+  double* Rv = (double*)r.R;
+  double* Pv = (double*)r.P;
+  double* Vv = (double*)r.V;
+  double* Tv = (double*)r.T;
+  unsigned* ctr = (unsigned*)r.ctr;
+  unsigned long long* gran = (unsigned long long*)r.gran;
+  unsigned* err = (unsigned*)r.err;
+  double* s_P = L.s_P;
+  int* s_A = L.s_A;
+  int* s_ex = L.s_ex;
+  int& s_flag = *L.s_flag;
+  int& s_stop = *L.s_stop;
+  const int n1 = n_a + 1;
+  // column passes: every lane of a wave takes part in every pass (the heavy sums need the
+  // whole wave), lanes past the own columns carry valid = false
+  const int npass = (n_own + TH - 1) / TH;
+
+  auto barrier = [&]() -> bool {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores have left
+    ++nb;
+    return hc_barrier(err, ctr, (unsigned)G * nb, &s_flag);
+  };
+  auto lo_at = [&](int s, int j) -> int {
+    const int* p = LO + (size_t)s * n_a + j;
+    return r.lottery_fresh ? __hip_atomic_load(to_global(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  };
+
+  // ---- setup: P; inverse lottery scatter of the own sources; exported bounds ----
+  for (int q = tid; q < SMAX * SMAX; q += TH) {
+    const int s = q / SMAX, sp = q - s * SMAX;
+    s_P[q] = (s < S && sp < S) ? ((const double*)r.Pc)[s * S + sp] : 0.0;
+  }
+  unsigned bad = 0u;
+  for (int q = tid; q < S * n_own; q += TH) {
+    const int s = q / n_own, j = j0 + (q - s * n_own);
+    const int l = lo_at(s, j);
+    const int lp = j > 0 ? lo_at(s, j - 1) : -1;
+    if (l < lp || l < 0 || l > n_a - 2) bad = 2u;
+    const int dhi = l < lp ? lp : l;
+    for (int d = lp + 1; d <= dhi; ++d) __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (j == n_a - 1)
+      for (int d = dhi + 1; d <= n_a; ++d)
+        __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), n_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // exported prefix [j0, ex0) (lo < j0) and suffix [ex1, j1) (lo + 1 >= j1) of each row
+  if (tid < S) {
+    const int s = tid;
+    int lo = j0, hi = j1;   // first own j with lo_j >= j0
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lo_at(s, mid) < j0) lo = mid + 1; else hi = mid;
+    }
+    s_ex[2 * s] = lo;
+    int lo2 = j0, hi2 = j1;   // first own j with lo_j + 1 >= j1
+    while (lo2 < hi2) {
+      const int mid = (lo2 + hi2) >> 1;
+      if (lo_at(s, mid) + 1 < j1) lo2 = mid + 1; else hi2 = mid;
+    }
+    s_ex[2 * s + 1] = lo2;
+  }
+  if (!barrier()) return -1;
+  if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  __syncthreads();
+  if (s_stop) return -1;
+  for (int q = tid; q < S * span; q += TH) {   // A(d) for d in [j0 - 1, j1] (A(-1) = 0)
+    const int s = q / span, d = j0 - 1 + (q - s * span);
+    s_A[s * span + (d - j0 + 1)] =
+        d < 0 ? 0 : __hip_atomic_load(to_global(&A[(size_t)s * n1 + d]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+
+  // stores of the vectors a matvec reads: write-through where another workgroup pulls them
+  auto put = [&](double* V, int s, int j, double v) {
+    double* p = V + (size_t)s * n_a + j;
+    if (j < s_ex[2 * s] || j >= s_ex[2 * s + 1]) store_f64_agent(p, v);
+    else *p = v;
+  };
+  auto q_at = [&](const double* Q, int s, int j) -> double {
+    const double* p = Q + (size_t)s * n_a + j;
+    return (j >= j0 && j < j1) ? *p : load_f64_agent(p);
+  };
+  auto w_at = [&](int s, int j) -> double {
+    const double* p = WL + (size_t)s * n_a + j;
+    return (r.lottery_fresh && (j < j0 || j >= j1)) ? load_f64_agent(p) : *p;
+  };
+  // T_s[d] of this lane's destination (valid lanes), the wave summing heavy destinations
+  auto pull = [&](const double* Q, int s, int d, bool valid) -> double {
+    const int* As = s_A + s * span - (j0 - 1);
+    const int a0 = valid ? As[d - 1] : 0, a1 = valid ? As[d] : 0, a2 = valid ? As[d + 1] : 0;
+    const bool heavy = valid && (a2 - a0) > kHpHeavy;
+    double acc = 0.0;
+    if (valid && !heavy) {
+      for (int j = a1; j < a2; ++j) acc += w_at(s, j) * q_at(Q, s, j);           // np.add.at(T, lo, w q)
+      for (int j = a0; j < a1; ++j) acc += (1.0 - w_at(s, j)) * q_at(Q, s, j);   // np.add.at(T, lo + 1, (1 - w) q)
+    }
+    unsigned long long hm = __ballot(heavy);
+    while (hm) {   // wave-uniform
+      const int h = __builtin_ctzll(hm);
+      hm &= hm - 1ull;
+      const int b0 = __builtin_amdgcn_readlane(a0, h), b1 = __builtin_amdgcn_readlane(a1, h),
+                b2 = __builtin_amdgcn_readlane(a2, h);
+      double pa = 0.0, pb = 0.0;
+      for (int j = b1 + lane; j < b2; j += kWave) pa += w_at(s, j) * q_at(Q, s, j);
+      for (int j = b0 + lane; j < b1; j += kWave) pb += (1.0 - w_at(s, j)) * q_at(Q, s, j);
+      const double ta = wave_sum_lane63(pa), tb = wave_sum_lane63(pb);
+      const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
+      if (lane == h) acc = tot;
+    }
+    return acc;
+  };
+  // out = T Q on every own point, handed to fuse(s', d, out) in column order
+  auto matvec = [&](const double* Q, auto&& fuse) -> bool {
+    if (!barrier()) return false;   // every workgroup's Q is in memory
+    for (int k = 0; k < npass; ++k) {
+      const int d = j0 + tid + k * TH;
+      const bool valid = d < j1;
+      double Tq[SMAX];
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) Tq[s] = s < S ? pull(Q, s, d, valid) : 0.0;
+      if (valid) {
+#pragma unroll
+        for (int sp = 0; sp < SMAX; ++sp) {
+          if (sp < S) {
+            double acc = 0.0;
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * Tq[s];   // (P.T @ T)[sp, d]
+            fuse(sp, d, acc);
+          }
+        }
+      }
+    }
+    return true;
+  };
+  // cluster-wide reduction (hist_bicg.h's protocol: tagged granules, fixed order)
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax) -> bool {
+#pragma unroll
+    for (int v = 0; v < kHkRed; ++v) {
+      if (v < nv) {
+        const double x = (kmax >> v) & 1u ? wave_nan_max(vals[v]) : wave_sum_lane63(vals[v]);
+        if (lane == kWave - 1) L.s_part[v][wid] = x;
+      }
+    }
+    __syncthreads();
+    ++ne;
+    const unsigned long long tag = (unsigned long long)ne << 32;
+    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
+    if (tid < nv) {
+      const int v = tid;
+      double x = L.s_part[v][0];
+      for (int q = 1; q < TH / kWave; ++q) x = (kmax >> v) & 1u ? nan_max(x, L.s_part[v][q]) : x + L.s_part[v][q];
+      const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+      unsigned long long* g = slot + (size_t)w * (2 * kHkRed) + 2 * v;
+      __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (wid == 0) {
+      double xa[kHkRed], xb[kHkRed];
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok;
+      do {
+        ok = true;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int w2 = lane + u * kWave;
+#pragma unroll
+          for (int v = 0; v < kHkRed; ++v) {
+            double x = 0.0;
+            if (v < nv && w2 < G) {
+              const unsigned long long* g = slot + (size_t)w2 * (2 * kHkRed) + 2 * v;
+              const unsigned long long hi = __hip_atomic_load(to_global(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long lo = __hip_atomic_load(to_global(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = ok && (hi & 0xffffffff00000000ull) == tag && (lo & 0xffffffff00000000ull) == tag;
+              x = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            }
+            if (u == 0) xa[v] = x;
+            else xb[v] = x;
+          }
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHcTimeoutTicks) {
+          if (lane == 0) __hip_atomic_store(to_global(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      } while (true);
+      if (lane == 0) s_flag = ok ? 1 : 0;
+#pragma unroll
+      for (int v = 0; v < kHkRed; ++v) {
+        if (v < nv) {
+          const bool mx = (kmax >> v) & 1u;
+          const double y = mx ? wave_nan_max(nan_max(xa[v], xb[v])) : wave_sum_lane63(xa[v] + xb[v]);
+          if (lane == kWave - 1) L.s_res[v] = y;
+        }
+      }
+    }
+    __syncthreads();
+    return s_flag != 0;
+  };
+  // every own point once (elementwise updates between the matvecs)
+  auto own_points = [&](auto&& f) {
+    for (int q = tid; q < S * n_own; q += TH) {
+      const int s = q / n_own, j = j0 + (q - s * n_own);
+      f(s, j, (size_t)s * n_a + j);
+    }
+  };
+
+  // ---- BiCGSTAB on (I - T) x = 0 (hist_bicg.h, the same recurrences and stopping rule) ----
+  double part[kHkRed];
+  const double tol = r.tol;
+  int mv = 0;
+  bool restart = true, first = true;
+  double rho = 0.0, total0 = 0.0;
+  unsigned seed = 0;
+  auto rh_at = [&](int s, int j) { return hk_rhat((unsigned)(s * n_a + j) + seed * 0x5BD1E995u); };
+  double best = __builtin_inf();
+  int mv_best = 0;
+  while (true) {
+    if (restart) {
+      // t = T x, r = t - x (p = r); the converged answer is t
+      double rr = 0.0, rm = 0.0, xs = 0.0;
+      if (!matvec(X, [&](int s, int j, double out) {
+            const size_t g = (size_t)s * n_a + j;
+            const double x = X[g];
+            const double rv = out - x;
+            Tv[g] = out;
+            put(Rv, s, j, rv);
+            put(Pv, s, j, rv);
+            rr += rh_at(s, j) * rv;
+            rm = nan_max(rm, fabs(rv));
+            xs += x;
+          }))
+        return -1;
+      ++mv;
+      part[0] = rr;
+      part[1] = rm;
+      part[2] = xs;
+      if (!reduce(part, 3, 2u)) return -1;
+      rho = L.s_res[0];
+      if (mv == 1) total0 = L.s_res[2];
+      if (L.s_res[1] < tol || mv >= r.max_iter) {
+        const double scale = total0 / L.s_res[2];
+        const bool one = mv == 1;
+        own_points([&](int s, int j, size_t g) { put(X, s, j, one ? Tv[g] : Tv[g] * scale); });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        break;
+      }
+      restart = false;
+      first = true;
+    }
+    if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
+      s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
+    // v = p - T p; alpha = rho / <rh, v>; max|r| rides along
+    double rvv = 0.0, rm = 0.0;
+    if (!matvec(Pv, [&](int s, int j, double out) {
+          const size_t g = (size_t)s * n_a + j;
+          const double v = Pv[g] - out;
+          Vv[g] = v;
+          rvv += rh_at(s, j) * v;
+          rm = nan_max(rm, fabs(Rv[g]));
+        }))
+      return -1;
+    ++mv;
+    part[0] = rvv;
+    part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
+    if (!reduce(part, 2, 2u)) return -1;
+    if (L.s_res[1] >= kHkStopSentinel) return -(2 + mv);
+    if ((!first && L.s_res[1] < tol) || mv >= r.max_iter) {
+      restart = true;
+      continue;
+    }
+    if (first || L.s_res[1] < 0.9 * best) {
+      best = first ? __builtin_inf() : L.s_res[1];
+      mv_best = mv;
+    } else if (mv - mv_best > kHkStall) {
+      ++seed;
+      best = __builtin_inf();
+      restart = true;
+      continue;
+    }
+    first = false;
+    const double alpha = rho / L.s_res[0];
+    if (!(fabs(alpha) < 1e300)) {
+      restart = true;
+      continue;
+    }
+    // s = r - alpha v (into R); x += alpha p
+    own_points([&](int s, int j, size_t g) {
+      put(Rv, s, j, Rv[g] - alpha * Vv[g]);
+      put(X, s, j, X[g] + alpha * Pv[g]);
+    });
+    // t = s - T s; omega = <t, s> / <t, t>
+    double ts = 0.0, tt = 0.0, rs = 0.0, rt = 0.0, sm = 0.0;
+    if (!matvec(Rv, [&](int s, int j, double out) {
+          const size_t g = (size_t)s * n_a + j;
+          const double sv = Rv[g];
+          const double t = sv - out;
+          Tv[g] = t;
+          const double h = rh_at(s, j);
+          ts += t * sv;
+          tt += t * t;
+          rs += h * sv;
+          rt += h * t;
+          sm = nan_max(sm, fabs(sv));
+        }))
+      return -1;
+    ++mv;
+    part[0] = ts;
+    part[1] = tt;
+    part[2] = rs;
+    part[3] = rt;
+    part[4] = sm;
+    if (!reduce(part, 5, 16u)) return -1;
+    double omega = (L.s_res[4] < tol) ? 0.0 : L.s_res[0] / L.s_res[1];
+    if (!(fabs(omega) < 1e300)) omega = 0.0;
+    if (omega == 0.0) {
+      restart = true;
+      continue;
+    }
+    const double rho2 = L.s_res[2] - omega * L.s_res[3];
+    const double beta = (rho2 / rho) * (alpha / omega);
+    rho = rho2;
+    // x += omega s; r = s - omega t; p = r + beta (p - omega v)
+    own_points([&](int s, int j, size_t g) {
+      const double sv = Rv[g], t = Tv[g];
+      put(X, s, j, X[g] + omega * sv);
+      const double rn = sv - omega * t;
+      put(Rv, s, j, rn);
+      put(Pv, s, j, rn + beta * (Pv[g] - omega * Vv[g]));
+    });
+    if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
+  }
+  return mv;
+}
+
+}  // namespace aiy

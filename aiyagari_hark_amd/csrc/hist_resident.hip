@@ -519,6 +519,7 @@ struct HcPlan {
   size_t vblock = 0;
   size_t lds = 0;
   const void* fn = nullptr;
+  bool pull = false;   // hist_pull.h form (S > 8 BiCGSTAB)
 };
 
 template <int SMAX, int KC, int TH>
@@ -536,6 +537,36 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
   if (S > 32 || S < 1 || n_a < 2) return false;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
+  if (krylov && S > 8) {   // pull form (hist_pull.h): vectors in HBM, every calibration at once
+    p.pull = true;
+    p.smax = 32;
+    p.th = kHpTH;
+    p.kc = 1;
+    p.cap = 0;
+    p.vblock = 0;
+    p.fn = hist_pull_pick(S);
+    if (!p.fn) return false;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
+    int lds_dev = 0;
+    if (hipDeviceGetAttribute(&lds_dev, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess)
+      return false;
+    const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
+    if (fa.sharedSizeBytes + 4096 >= lds_total) return false;
+    const size_t budget = lds_total - fa.sharedSizeBytes - 1024;
+    const int max_own = (int)(budget / (sizeof(int) * (size_t)S)) - 2;
+    if (max_own < 1) return false;
+    const int g_min = (n_a + max_own - 1) / max_own;
+    if (g_min > kHcMaxG || g_min > cus) return false;
+    const int g_cap = h->hist_cluster_cap > 0 ? h->hist_cluster_cap : kHcMaxG;
+    int G = std::max(g_min, std::min(std::min(g_cap, kHcMaxG), cus / std::max(1, n_cal)));
+    G = std::min(G, n_a);
+    p.nj = (n_a + G - 1) / G;
+    p.G = (n_a + p.nj - 1) / p.nj;
+    p.cals_per_launch = std::max(1, cus / p.G);
+    p.lds = (hist_pull_lds(S, p.nj) + 255) / 256 * 256;
+    return p.lds <= budget;
+  }
   p.smax = S <= 8 ? 8 : (S <= 16 ? 16 : 32);
   const int kc_max = p.smax == 8 ? 2 : 1;
   p.th = 512;
@@ -625,7 +656,20 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   off += (size_t)per_launch * 2 * p.G * kHcRedRec * sizeof(double);
   r.accel = krylov ? 0 : h->hist_accel;
   r.dbuf = nullptr;
-  if (r.accel > 0 || krylov) {   // Aitken: stored differences; BiCGSTAB: the p scratch rows
+  r.ainv = nullptr;
+  if (p.pull) {   // pull form: four [S][n_a] vectors per calibration + the inverse lottery
+    const size_t vb = (size_t)n_cal * 4 * S * n_a * sizeof(double);
+    const size_t db = vb + (size_t)n_cal * S * (n_a + 1) * sizeof(int);
+    if (db > h->hc_dcap) {
+      if (h->d_hcd) (void)hipFree(h->d_hcd);
+      h->d_hcd = nullptr;
+      h->hc_dcap = 0;
+      AIY_HIP(h, hipMalloc(&h->d_hcd, db));
+      h->hc_dcap = db;
+    }
+    r.dbuf = static_cast<double*>(h->d_hcd);
+    r.ainv = reinterpret_cast<int*>(static_cast<char*>(h->d_hcd) + vb);
+  } else if (r.accel > 0 || krylov) {   // Aitken: stored differences; BiCGSTAB: the p scratch rows
     if (r.accel > 0 && r.accel < 4) r.accel = 4;
     const size_t db = ((size_t)n_cal * S * n_a + (size_t)per_launch * p.G * p.vblock) * sizeof(double);
     if (db > h->hc_dcap) {

@@ -158,3 +158,31 @@ def test_bicgstab_histogram_matches_oracle(gpu):
     assert abs(K[0] - Ke) / Ke < 1e-6, (K[0], Ke)
     plain, iters_p, _ = ST.stationary_hist(lo, wlo, P, aGrid.size, tol=1e-12, step=ST.hist_step_fast)
     assert int(it[0]) * 3 < iters_p, (int(it[0]), iters_p)
+
+
+def test_pull_bicgstab_stress_size(gpu):
+    """The pull form (csrc/hist_pull.h) that solves S > 8 calibrations: the three configs[4]
+    cells (25-state Rouwenhorst, N_a = 50 000) in ONE launch near their roots.  Against the
+    oracle's transition on the same policies: residual max|T m - m| at the plain rule's
+    level, total mass 1; a second solve from the same start is bit-identical (no atomics)."""
+    from aiyagari_hark_amd.stationary import Calibration
+    from oracle import stationary as ST
+    cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst")
+            for c in (1.0, 3.0, 5.0)]
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 50000, 2)
+    r = np.array([0.038, 0.028, 0.017])
+    _launches(gpu)
+    K, it, m, b = _solve(gpu, cals, aGrid, r, True, accel=-1)
+    n = _launches(gpu)
+    assert n == 1, f"{n} launches: the three clusters should be co-resident"
+    K2, it2, m2, _ = _solve(gpu, cals, aGrid, r, True, accel=-1)
+    assert np.array_equal(it, it2) and np.array_equal(m, m2), "pull-form solve not reproducible"
+    for c, cal in enumerate(cals):
+        lab, P = ST.income_process(25, cal.LaborAR, cal.LaborSD, "rouwenhorst")
+        w, _ = ST.prices(r[c], 0.36, 0.08)
+        mt, ct = (x[c].cpu().numpy() for x in b.last_tables)
+        lo, wlo, _ = ST.savings_lottery(mt[:, 0], ct[:, 0], aGrid, 1.0 + r[c], w, lab)
+        res = np.max(np.abs(ST.hist_step_fast(m[c], lo, wlo, P) - m[c]))
+        print(f"\ncell {c}: {int(it[c])} matvecs, residual {res:.2e}, K {K[c]:.6f}")
+        assert res < 1e-11, res
+        assert abs(m[c].sum() - 1.0) < 1e-10
