@@ -150,6 +150,15 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     s_A[s * span + (d - j0 + 1)] =
         d < 0 ? 0 : __hip_atomic_load(to_global(&A[(size_t)s * n1 + d]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // the start x may have been stored plain by its owner in this launch (the GE search's warm
+  // start): its exported entries are written through before the first matvec's barrier
+  for (int q = tid; q < S * n_own; q += TH) {
+    const int s = q / n_own, j = j0 + (q - s * n_own);
+    if (j < s_ex[2 * s] || j >= s_ex[2 * s + 1]) {
+      double* p = X + (size_t)s * n_a + j;
+      store_f64_agent(p, *p);
+    }
+  }
   __syncthreads();
 
   // stores of the vectors a matvec reads: write-through where another workgroup pulls them
@@ -158,38 +167,65 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     if (j < s_ex[2 * s] || j >= s_ex[2 * s + 1]) store_f64_agent(p, v);
     else *p = v;
   };
-  auto q_at = [&](const double* Q, int s, int j) -> double {
-    const double* p = Q + (size_t)s * n_a + j;
-    return (j >= j0 && j < j1) ? *p : load_f64_agent(p);
-  };
+  // source loads: sc1 (L2-served) for every source, own or foreign -- own plain stores are in
+  // the own L2, foreign ones were written through (no per-lane branch between load kinds)
+  auto q_at = [&](const double* Q, int s, int j) -> double { return load_f64_agent(Q + (size_t)s * n_a + j); };
   auto w_at = [&](int s, int j) -> double {
     const double* p = WL + (size_t)s * n_a + j;
-    return (r.lottery_fresh && (j < j0 || j >= j1)) ? load_f64_agent(p) : *p;
+    return r.lottery_fresh ? load_f64_agent(p) : *p;
   };
-  // T_s[d] of this lane's destination (valid lanes), the wave summing heavy destinations
-  auto pull = [&](const double* Q, int s, int d, bool valid) -> double {
-    const int* As = s_A + s * span - (j0 - 1);
-    const int a0 = valid ? As[d - 1] : 0, a1 = valid ? As[d] : 0, a2 = valid ? As[d + 1] : 0;
-    const bool heavy = valid && (a2 - a0) > kHpHeavy;
-    double acc = 0.0;
-    if (valid && !heavy) {
-      for (int j = a1; j < a2; ++j) acc += w_at(s, j) * q_at(Q, s, j);           // np.add.at(T, lo, w q)
-      for (int j = a0; j < a1; ++j) acc += (1.0 - w_at(s, j)) * q_at(Q, s, j);   // np.add.at(T, lo + 1, (1 - w) q)
+  // T_s[d] for the rows s0 .. s0 + GRP of this lane's destination d: the first two sources of
+  // each part (lo = d: w q; lo = d - 1: (1 - w) q) loaded for all rows of the group at once
+  // (clamped indices, unconditional), further sources in a loop (rare), a destination with
+  // more than kHpHeavy sources by its whole wave
+  constexpr int GRP = 4;
+  auto pull_group = [&](const double* Q, int s0, int d, bool valid, double (&Tq)[SMAX]) {
+    int a0[GRP], a1[GRP], a2[GRP];
+    double wv[GRP][4], qv[GRP][4];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u) {
+      const int s = s0 + u < S ? s0 + u : S - 1;
+      const int* As = s_A + s * span - (j0 - 1);
+      a0[u] = valid ? As[d - 1] : 0;
+      a1[u] = valid ? As[d] : 0;
+      a2[u] = valid ? As[d + 1] : 0;
+      const int i0 = min(a1[u], n_a - 1), i1 = min(a1[u] + 1, n_a - 1);
+      const int i2 = min(a0[u], n_a - 1), i3 = min(a0[u] + 1, n_a - 1);
+      wv[u][0] = w_at(s, i0); qv[u][0] = q_at(Q, s, i0);
+      wv[u][1] = w_at(s, i1); qv[u][1] = q_at(Q, s, i1);
+      wv[u][2] = w_at(s, i2); qv[u][2] = q_at(Q, s, i2);
+      wv[u][3] = w_at(s, i3); qv[u][3] = q_at(Q, s, i3);
     }
-    unsigned long long hm = __ballot(heavy);
-    while (hm) {   // wave-uniform
-      const int h = __builtin_ctzll(hm);
-      hm &= hm - 1ull;
-      const int b0 = __builtin_amdgcn_readlane(a0, h), b1 = __builtin_amdgcn_readlane(a1, h),
-                b2 = __builtin_amdgcn_readlane(a2, h);
-      double pa = 0.0, pb = 0.0;
-      for (int j = b1 + lane; j < b2; j += kWave) pa += w_at(s, j) * q_at(Q, s, j);
-      for (int j = b0 + lane; j < b1; j += kWave) pb += (1.0 - w_at(s, j)) * q_at(Q, s, j);
-      const double ta = wave_sum_lane63(pa), tb = wave_sum_lane63(pb);
-      const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
-      if (lane == h) acc = tot;
+#pragma unroll
+    for (int u = 0; u < GRP; ++u) {
+      const int s = s0 + u;
+      if (s >= S) break;   // wave-uniform
+      const int n1c = a2[u] - a1[u], n0c = a1[u] - a0[u];
+      const bool heavy = valid && (n1c + n0c) > kHpHeavy;
+      double acc = 0.0;
+      if (valid && !heavy) {
+        if (n1c > 0) acc += wv[u][0] * qv[u][0];                     // np.add.at(T, lo, w q), ascending j
+        if (n1c > 1) acc += wv[u][1] * qv[u][1];
+        for (int j = a1[u] + 2; j < a2[u]; ++j) acc += w_at(s, j) * q_at(Q, s, j);
+        if (n0c > 0) acc += (1.0 - wv[u][2]) * qv[u][2];             // np.add.at(T, lo + 1, (1 - w) q)
+        if (n0c > 1) acc += (1.0 - wv[u][3]) * qv[u][3];
+        for (int j = a0[u] + 2; j < a1[u]; ++j) acc += (1.0 - w_at(s, j)) * q_at(Q, s, j);
+      }
+      unsigned long long hm = __ballot(heavy);
+      while (hm) {   // wave-uniform
+        const int h = __builtin_ctzll(hm);
+        hm &= hm - 1ull;
+        const int b0 = __builtin_amdgcn_readlane(a0[u], h), b1 = __builtin_amdgcn_readlane(a1[u], h),
+                  b2 = __builtin_amdgcn_readlane(a2[u], h);
+        double pa = 0.0, pb = 0.0;
+        for (int j = b1 + lane; j < b2; j += kWave) pa += w_at(s, j) * q_at(Q, s, j);
+        for (int j = b0 + lane; j < b1; j += kWave) pb += (1.0 - w_at(s, j)) * q_at(Q, s, j);
+        const double ta = wave_sum_lane63(pa), tb = wave_sum_lane63(pb);
+        const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
+        if (lane == h) acc = tot;
+      }
+      Tq[s] = acc;
     }
-    return acc;
   };
   // out = T Q on every own point, handed to fuse(s', d, out) in column order
   auto matvec = [&](const double* Q, auto&& fuse) -> bool {
@@ -199,7 +235,11 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       const bool valid = d < j1;
       double Tq[SMAX];
 #pragma unroll
-      for (int s = 0; s < SMAX; ++s) Tq[s] = s < S ? pull(Q, s, d, valid) : 0.0;
+      for (int s = 0; s < SMAX; ++s) Tq[s] = 0.0;
+#pragma unroll
+      for (int s0 = 0; s0 < SMAX; s0 += GRP) {
+        if (s0 < S) pull_group(Q, s0, d, valid, Tq);
+      }
       if (valid) {
 #pragma unroll
         for (int sp = 0; sp < SMAX; ++sp) {

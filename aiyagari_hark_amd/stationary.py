@@ -364,7 +364,7 @@ def _solve_groups(cals, aGrid, dev, groups, method, r_tol, egm_tol, hist_tol, ma
         if key not in _GROUP_CTX:
             _GROUP_CTX[key] = (_lib.Handle(dev.index), torch.cuda.Stream(dev))
         h, st = _GROUP_CTX[key]
-        h.set_options(dict(carry, **{_lib.AIY_OPT_HIST_CLUSTER: cap}))
+        h.set_options({**carry, _lib.AIY_OPT_HIST_CLUSTER: cap})
         b = StationaryBatch([cals[i] for i in ii], aGrid, device=dev)
         sub = lambda x: None if x is None else np.broadcast_to(np.asarray(x, float), (n,))[ii]  # noqa: E731
         st.wait_stream(cur)

@@ -46,6 +46,8 @@ for step in "$@"; do
     hphase_t2) run hphase_t2 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/hist_phases.py 24 0 -1 ;;
     trace_c4) export TMPDIR=/tmp; run trace_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c4 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --legs configs4 ;;
     trace_c3) export TMPDIR=/tmp; run trace_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c3 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs3 ;;
+    pull) run pull 400 $PYT -s tests/test_gpu_hist_resident.py -k "pull or rouwenhorst" ;;
+    c4) run c4 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
