@@ -40,6 +40,7 @@ AIY_OPT_CU_LIMIT = 11
 AIY_OPT_GE_REBALANCE = 12
 AIY_OPT_GE_EXTRAP_PERIOD = 13
 AIY_OPT_GE_LOGSEC = 14
+AIY_OPT_HIST_PULL = 15
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

@@ -75,6 +75,9 @@ struct GeRun {
   int warm_hist, warm_egm, secant, loose, extrap;
   int extrap_period;      // EGM cycles between extrapolation checks (>= 4)
   int logsec;             // log-secant bracketing (AIY_OPT_GE_LOGSEC, with loose bracketing)
+  int pull;               // distribution solves by the lottery pull (AIY_OPT_HIST_PULL): deterministic
+  double* qb;             // [n_cal][S][n_a] pull form: the matvec input rows
+  int* ainv;              // [n_cal][S][n_a + 1] pull form: inverse lottery
   double* tab;            // [n_cal][kGeBufs][2][S][n_a + 1]
   double* mass;           // [n_cal][S][n_a]
   double* pmass;          // [n_cal][S][n_a] previous evaluation's mass
@@ -385,7 +388,8 @@ __device__ __forceinline__ double ge_egm_cycle_fn(int S, int n_a, int j0, int j1
 // lottery of the own columns on the final tables (hist.hip hist_lottery_kernel's arithmetic)
 template <int SMAX, int NW>
 __device__ __forceinline__ void ge_lottery_fn(int S, int n_a, int j0, int j1, const double* a_grid, const double* fm,
-                                           const double* fc, double R, bool have_prev, int* LO, double* WL) {
+                                           const double* fc, double R, bool have_prev, int* LO, double* WL,
+                                           bool write_through) {
   ge_rows_pass<SMAX, NW>(S, n_a, j0, j1, a_grid, fm, fc, R, ge_s_Wl, ge_s_hint, ge_dyn + (size_t)NW * SMAX * kTile,
                      [&](int, int jr, int, int s, double q, double c) {
                        if (jr >= j1) return;
@@ -407,8 +411,13 @@ __device__ __forceinline__ void ge_lottery_fn(int S, int n_a, int j0, int j1, co
                        d = d < 0 ? 0 : (d > n_a - 2 ? n_a - 2 : d);
                        double wl = (a_grid[d + 1] - ap) / (a_grid[d + 1] - a_grid[d]);
                        wl = wl < 0.0 ? 0.0 : (wl > 1.0 ? 1.0 : wl);
-                       LO[o] = d;
-                       WL[o] = wl;
+                       if (write_through) {   // the pull form reads foreign lottery entries
+                         __hip_atomic_store(to_global(&LO[o]), d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                         store_f64_agent(&WL[o], wl);
+                       } else {
+                         LO[o] = d;
+                         WL[o] = wl;
+                       }
                      },
                      [](int, int) {}, [](int, int, double) {});
 }
@@ -697,7 +706,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       __syncthreads();
       // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
       tp = __builtin_amdgcn_s_memrealtime();
-      ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL);
+      ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL,
+                              g.pull != 0);
       // ---- the distribution's start (own columns) ----
       if (st.fresh_mass) {
         const double u0 = 1.0 / ((double)S * n_a);
@@ -733,7 +743,10 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.tol = st.htol;
       hk.stop_ctr = to_global((const unsigned*)(g.stop_at > 0 ? g.done_ctr : nullptr));
       hk.stop_at = (unsigned)g.stop_at;
-      mv = hk_solve_isolated<SMAX, KC, TH>(hk, &nb, &ne);
+      hk.Qg = to_global(g.qb + row0);
+      hk.Ainv = to_global(g.ainv + (size_t)cal * S * (n_a + 1));
+      hk.lottery_fresh = true;
+      mv = g.pull ? hk_solve_isolated<SMAX, KC, TH, true>(hk, &nb, &ne) : hk_solve_isolated<SMAX, KC, TH, false>(hk, &nb, &ne);
     }
     if (mv == -1) return;
     if (tid == 0) {
@@ -875,7 +888,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
+  size_t tab, mass, pmass, pg, qb, ainv, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
       evlog, bytes;
 };
 // Per-calibration arrays (kept across the rebalancing launches) first, then the per-launch
@@ -887,7 +900,8 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_m
   auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) / 256 * 256; return at; };
   const size_t pts = (size_t)n_cal * S * n_a;
   L.tab = take((size_t)n_cal * kGeBufs * 2 * S * (n_a + 1) * sizeof(double));
-  L.mass = take(pts * 8); L.pmass = take(pts * 8); L.pg = take(pts * 8);
+  L.mass = take(pts * 8); L.pmass = take(pts * 8); L.pg = take(pts * 8); L.qb = take(pts * 8);
+  L.ainv = take((size_t)n_cal * S * (n_a + 1) * sizeof(int));
   L.lo = take(pts * 4); L.wlo = take(pts * 8);
   L.slab = take((size_t)cus * 2 * cap_max * sizeof(double));
   L.span = take((size_t)cus * 8 * 4 * sizeof(int));
@@ -957,6 +971,9 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.mass = reinterpret_cast<double*>(base + L.mass);
   g.pmass = reinterpret_cast<double*>(base + L.pmass);
   g.pg = reinterpret_cast<double*>(base + L.pg);
+  g.qb = reinterpret_cast<double*>(base + L.qb);
+  g.ainv = reinterpret_cast<int*>(base + L.ainv);
+  g.pull = h->hist_pull;
   g.lo = reinterpret_cast<int*>(base + L.lo);
   g.wlo = reinterpret_cast<double*>(base + L.wlo);
   g.slab = reinterpret_cast<double*>(base + L.slab);

@@ -58,6 +58,7 @@ struct HkShared {
   double* s_res;                   // [kHkRed]
   int* s_flag;
   int* s_stop;
+  int* s_ex;                       // [SMAX][2] pull form: exported prefix / suffix of the own sources
 };
 
 // One calibration's BiCGSTAB distribution solve by the workgroups of its cluster (this
@@ -84,6 +85,11 @@ struct HkArgs {
   // (nullptr: never); the solve then returns -(2 + matvecs) with X a valid iterate
   gptr<const unsigned> stop_ctr;
   unsigned stop_at;
+  // pull form of the matvec (PULL = true, hist_pull.h's lottery pull with the vectors kept in
+  // registers): the matvec input staged in Qg, the inverse lottery in Ainv
+  gptr<double> Qg;             // [S][n_a]
+  gptr<int> Ainv;              // [S][n_a + 1]
+  bool lottery_fresh;          // LO / WL written in this launch by other workgroups (sc1 loads)
 };
 
 // Returns the matvecs of the solve, or -1 when the cluster stops (error word set: a
@@ -91,7 +97,7 @@ struct HkArgs {
 // a rebalancing stop was requested (X holds the current iterate; a later solve restarts
 // from it).  nb / ne: the
 // cluster barriers / reductions passed so far in this launch (counted on).
-template <int SMAX, int KC, int TH>
+template <int SMAX, int KC, int TH, bool PULL = false>
 __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
                                         unsigned& ne) {
   constexpr bool kVlds = SMAX <= 8;
@@ -132,7 +138,65 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     const int s = q / SMAX, sp = q - s * SMAX;
     s_P[q] = (s < S && sp < S) ? Pc[s * S + sp] : 0.0;
   }
-  if (tid == 0) {
+  auto barrier = [&]() -> bool {
+    ++nb;
+    return hc_barrier(err, ctr, (unsigned)G * nb, &s_flag);
+  };
+  // pull form: the inverse lottery of the own destinations, staged in LDS (Tacc's space)
+  const int n_own = j1 - j0, aspan = n_own + 2;
+  int* s_A = reinterpret_cast<int*>(Tacc);
+  int* s_ex = L.s_ex;
+  int* Ainv = (int*)r.Ainv;
+  double* Qg = (double*)r.Qg;
+  auto lo_at = [&](int s, int j) -> int {
+    const int* p = LO + (size_t)s * n_a + j;
+    return r.lottery_fresh ? __hip_atomic_load(to_global(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  };
+  if constexpr (PULL) {
+    const int n1 = n_a + 1;
+    unsigned bad = 0u;
+    for (int q = tid; q < S * n_own; q += TH) {
+      const int s = q / n_own, j = j0 + (q - s * n_own);
+      const int l = lo_at(s, j);
+      const int lp = j > 0 ? lo_at(s, j - 1) : -1;
+      if (l < lp || l < 0 || l > n_a - 2) bad = 2u;
+      const int dhi = l < lp ? lp : l;
+      for (int d = lp + 1; d <= dhi; ++d)
+        __hip_atomic_store(to_global(&Ainv[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j == n_a - 1)
+        for (int d = dhi + 1; d <= n_a; ++d)
+          __hip_atomic_store(to_global(&Ainv[(size_t)s * n1 + d]), n_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (S * aspan * (int)sizeof(int) > cap * (int)sizeof(double)) bad = 2u;
+    if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < S) {   // exported prefix [j0, ex0) (lo < j0) and suffix [ex1, j1) (lo + 1 >= j1)
+      const int s = tid;
+      int lo = j0, hi = j1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (lo_at(s, mid) < j0) lo = mid + 1; else hi = mid;
+      }
+      s_ex[2 * s] = lo;
+      int lo2 = j0, hi2 = j1;
+      while (lo2 < hi2) {
+        const int mid = (lo2 + hi2) >> 1;
+        if (lo_at(s, mid) + 1 < j1) lo2 = mid + 1; else hi2 = mid;
+      }
+      s_ex[2 * s + 1] = lo2;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!barrier()) return -1;
+    if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    __syncthreads();
+    if (s_stop) return -1;
+    for (int q = tid; q < S * aspan; q += TH) {   // A(d) for d in [j0 - 1, j1] (A(-1) = 0)
+      const int s = q / aspan, d = j0 - 1 + (q - s * aspan);
+      s_A[q] = d < 0 ? 0 : __hip_atomic_load(to_global(&Ainv[(size_t)s * n1 + d]), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  if (!PULL && tid == 0) {
     int tot = 0;
     unsigned bad = 0;
     for (int s = 0; s < S; ++s) {
@@ -156,10 +220,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  auto barrier = [&]() -> bool {
-    ++nb;
-    return hc_barrier(err, ctr, (unsigned)G * nb, &s_flag);
-  };
+  if (!PULL) {
   if (!barrier()) return -1;
   if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
@@ -190,8 +251,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   if (tid == 0) s_stop = __hip_atomic_load(to_global(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   __syncthreads();
   if (s_stop) return -1;
+  }   // !PULL setup
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
+    if (PULL) break;
     const int d = j0 + tid + k * TH;
 #pragma unroll
     for (int s = 0; s < SMAX; ++s) {
@@ -402,8 +465,117 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       }
     }
   };
+  // pull form: q of the own points staged in Qg (the exported entries write-through), one
+  // cluster barrier, then every own destination pulls its sources (hist_pull.h)
+  auto stage_q = [&](const double (&q)[KC][SMAX]) {
+    const int jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = jc + k * TH;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        if (s < S && j < j1) {
+          double* p = Qg + (size_t)s * n_a + j;
+          if (j < s_ex[2 * s] || j >= s_ex[2 * s + 1]) store_f64_agent(p, q[k][s]);
+          else *p = q[k][s];
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto w_at = [&](int s, int j) -> double {
+    const double* p = WL + (size_t)s * n_a + j;
+    return r.lottery_fresh ? load_f64_agent(p) : *p;
+  };
+  auto q_at = [&](int s, int j) -> double { return load_f64_agent(Qg + (size_t)s * n_a + j); };
+  auto pull_mix = [&](double (&out)[KC][SMAX]) {
+    const int jc = col();
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      asm volatile("" ::: "memory");   // one column's loads at a time (else both are hoisted: spills)
+      const int d = jc + k * TH;
+      const bool valid = d < j1;
+      double T[SMAX];
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) T[s] = 0.0;
+      constexpr int GRP = SMAX <= 8 ? (KC == 1 ? (SMAX + 1) / 2 : 2) : 4;
+#pragma unroll
+      for (int s0 = 0; s0 < SMAX; s0 += GRP) {
+        if (s0 >= S) break;   // wave-uniform
+        asm volatile("" ::: "memory");
+        int a0[GRP], a1[GRP], a2[GRP];
+        double wv[GRP][4], qv[GRP][4];
+#pragma unroll
+        for (int u = 0; u < GRP; ++u) {
+          const int sc = min(s0 + u, S - 1);
+          const int* As = s_A + sc * aspan - (j0 - 1);
+          a0[u] = valid ? As[d - 1] : 0;
+          a1[u] = valid ? As[d] : 0;
+          a2[u] = valid ? As[d + 1] : 0;
+          const int i0 = min(a1[u], n_a - 1), i1 = min(a1[u] + 1, n_a - 1);
+          const int i2 = min(a0[u], n_a - 1), i3 = min(a0[u] + 1, n_a - 1);
+          wv[u][0] = w_at(sc, i0); qv[u][0] = q_at(sc, i0);
+          wv[u][1] = w_at(sc, i1); qv[u][1] = q_at(sc, i1);
+          wv[u][2] = w_at(sc, i2); qv[u][2] = q_at(sc, i2);
+          wv[u][3] = w_at(sc, i3); qv[u][3] = q_at(sc, i3);
+        }
+#pragma unroll
+        for (int u = 0; u < GRP; ++u) {
+          const int sr = s0 + u;
+          if (sr < S) {   // wave-uniform
+            const int n1c = a2[u] - a1[u], n0c = a1[u] - a0[u];
+            const bool heavy = valid && (n1c + n0c) > kWave;
+            double acc = 0.0;
+            if (valid && !heavy) {
+              if (n1c > 0) acc += wv[u][0] * qv[u][0];                    // np.add.at(T, lo, w q), ascending j
+              if (n1c > 1) acc += wv[u][1] * qv[u][1];
+              for (int j = a1[u] + 2; j < a2[u]; ++j) acc += w_at(sr, j) * q_at(sr, j);
+              if (n0c > 0) acc += (1.0 - wv[u][2]) * qv[u][2];            // np.add.at(T, lo + 1, (1 - w) q)
+              if (n0c > 1) acc += (1.0 - wv[u][3]) * qv[u][3];
+              for (int j = a0[u] + 2; j < a1[u]; ++j) acc += (1.0 - w_at(sr, j)) * q_at(sr, j);
+            }
+            unsigned long long hm = __ballot(heavy);
+            while (hm) {   // a destination with many sources: its whole wave, fixed order
+              const int h = __builtin_ctzll(hm);
+              hm &= hm - 1ull;
+              const int b0 = __builtin_amdgcn_readlane(a0[u], h), b1 = __builtin_amdgcn_readlane(a1[u], h),
+                        b2 = __builtin_amdgcn_readlane(a2[u], h);
+              double pa = 0.0, pb = 0.0;
+              for (int j = b1 + lane; j < b2; j += kWave) pa += w_at(sr, j) * q_at(sr, j);
+              for (int j = b0 + lane; j < b1; j += kWave) pb += (1.0 - w_at(sr, j)) * q_at(sr, j);
+              const double ta = wave_sum_lane63(pa), tb = wave_sum_lane63(pb);
+              const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
+              if (lane == h) acc = tot;
+            }
+            T[sr] = acc;
+          }
+        }
+      }
+#pragma unroll
+      for (int sp = 0; sp < SMAX; ++sp) {
+        double pc[SMAX];
+        asm volatile("" ::: "memory");   // one column of P at a time
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) pc[s] = s_P[s * SMAX + sp];
+        double acc = 0.0;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) acc += pc[s] * T[s];
+        out[k][sp] = acc;
+      }
+    }
+  };
   // one matvec: out = T q (the cluster exchange in the middle)
   auto matvec = [&](const double (&q)[KC][SMAX], double (&out)[KC][SMAX]) -> bool {
+    if constexpr (PULL) {
+      HK_PH(5);
+      stage_q(q);
+      HK_PH(1);
+      if (!barrier()) return false;
+      HK_PH(2);
+      pull_mix(out);
+      HK_PH(3);
+      return true;
+    }
     HK_PH(5);
     push(q);
     HK_PH(0);
@@ -717,7 +889,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 // carries a lot of live state of its own (ge_resident.hip's search loop) would otherwise
 // force the solve's registers into scratch; the call costs a few register saves per
 // solve.  The span buffer / v share the caller's dynamic LDS.
-template <int SMAX, int KC, int TH>
+template <int SMAX, int KC, int TH, bool PULL = false>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn[];
   __shared__ int s_base[SMAX];
@@ -730,10 +902,11 @@ __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigne
   __shared__ double s_part[kHkRed][TH / kWave];
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
+  __shared__ int s_ex[2 * SMAX];
   const HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop};
+                                 &s_flag, &s_stop, s_ex};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;

@@ -138,7 +138,7 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
 
 // BiCGSTAB form of the cluster kernel (hist_krylov.hip) for (S, padded S, columns per
 // thread) and its state count (*smax_k); nullptr when there is no instantiation
-const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k);
+const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k, bool pull = false);
 // pull form (hist_pull.h) for S > 8: the kernel, and its dynamic LDS for n_own columns
 const void* hist_pull_pick(int S);
 size_t hist_pull_lds(int S, int n_own);

@@ -40,7 +40,7 @@
 
 namespace aiy {
 
-template <int SMAX, int KC, int TH>
+template <int SMAX, int KC, int TH, bool PULL>
 __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   extern __shared__ double Tacc[];
   __shared__ int s_base[SMAX];
@@ -53,8 +53,9 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   __shared__ double s_part[kHkRed][TH / kWave];
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
+  __shared__ int s_ex[2 * SMAX];
   const HkShared<SMAX, KC, TH> L{Tacc, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop};
+                                 &s_flag, &s_stop, s_ex};
   const int G = r.G, S = r.S, n_a = r.n_a;
   const int lc = blockIdx.x / G;
   const int w = blockIdx.x - lc * G;
@@ -79,8 +80,12 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   a.err = to_global(r.err);
   a.stop_ctr = to_global((const unsigned*)nullptr);
   a.stop_at = 0u;
+  // pull form: the matvec input rows and the inverse lottery behind the p rows
+  a.Qg = to_global(PULL ? r.dbuf + (size_t)r.n_cal * S * n_a + row0 * n_a : (double*)nullptr);
+  a.Ainv = to_global(PULL ? r.ainv + (size_t)cal * S * (n_a + 1) : (int*)nullptr);
+  a.lottery_fresh = false;   // the lottery launch ran before this one
   unsigned nb = 0, ne = 0;
-  const int mv = hk_solve<SMAX, KC, TH>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
 }
 
@@ -135,15 +140,19 @@ const void* hist_pull_pick(int S) {
 }
 size_t hist_pull_lds(int S, int n_own) { return hp_lds_a_bytes<1>(n_own) * (size_t)S; }
 
-template <int SMAX, int KC, int TH>
+template <int SMAX, int KC, int TH, bool PULL = false>
 static const void* hk_fn() {
-  return reinterpret_cast<const void*>(hist_bicg_kernel<SMAX, KC, TH>);
+  return reinterpret_cast<const void*>(hist_bicg_kernel<SMAX, KC, TH, PULL>);
 }
 
 // kernel for the plan's (S, padded S, columns per thread) and its state count SMAX
-// (*smax_k); nullptr when there is no instantiation
-const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k) {
+// (*smax_k); nullptr when there is no instantiation.  pull: the lottery-pull matvec (S <= 8)
+const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k, bool pull) {
   *smax_k = smax;
+  if (pull && smax == 8) {
+    if (S == 7) return *smax_k = 7, (kc == 1 ? hk_fn<7, 1, 512, true>() : hk_fn<7, 2, 512, true>());
+    return kc == 1 ? hk_fn<8, 1, 512, true>() : hk_fn<8, 2, 512, true>();
+  }
   if (S == 7 && kc == 2) return *smax_k = 7, hk_fn<7, 2, 512>();
   if (smax == 8) return kc == 1 ? hk_fn<8, 1, 512>() : hk_fn<8, 2, 512>();
   if (kc != 1) return nullptr;

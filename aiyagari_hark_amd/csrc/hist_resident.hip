@@ -520,6 +520,7 @@ struct HcPlan {
   size_t lds = 0;
   const void* fn = nullptr;
   bool pull = false;   // hist_pull.h form (S > 8 BiCGSTAB)
+  bool pull_small = false;   // hk_solve's pull matvec (S <= 8, AIY_OPT_HIST_PULL)
 };
 
 template <int SMAX, int KC, int TH>
@@ -581,7 +582,8 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
   if (p.kc > kc_max) return false;
   p.cals_per_launch = std::max(1, cus / p.G);
   int smax_k = p.smax;
-  p.fn = krylov ? hist_bicg_pick(S, p.smax, p.kc, &smax_k) : hc_pick(p.smax, p.kc);
+  p.fn = krylov ? hist_bicg_pick(S, p.smax, p.kc, &smax_k, h->hist_pull != 0) : hc_pick(p.smax, p.kc);
+  p.pull_small = krylov && h->hist_pull != 0 && p.smax == 8;
   if (!p.fn) return false;
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
@@ -671,7 +673,10 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
     r.ainv = reinterpret_cast<int*>(static_cast<char*>(h->d_hcd) + vb);
   } else if (r.accel > 0 || krylov) {   // Aitken: stored differences; BiCGSTAB: the p scratch rows
     if (r.accel > 0 && r.accel < 4) r.accel = 4;
-    const size_t db = ((size_t)n_cal * S * n_a + (size_t)per_launch * p.G * p.vblock) * sizeof(double);
+    // p rows (+ v blocks); pull form: + the matvec input rows and the inverse lottery
+    const size_t dvec = ((size_t)n_cal * S * n_a * (p.pull_small ? 2 : 1) + (size_t)per_launch * p.G * p.vblock) *
+                        sizeof(double);
+    const size_t db = dvec + (p.pull_small ? (size_t)n_cal * S * (n_a + 1) * sizeof(int) : 0);
     if (db > h->hc_dcap) {
       if (h->d_hcd) (void)hipFree(h->d_hcd);
       h->d_hcd = nullptr;
@@ -680,6 +685,7 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
       h->hc_dcap = db;
     }
     r.dbuf = static_cast<double*>(h->d_hcd);
+    if (p.pull_small) r.ainv = reinterpret_cast<int*>(static_cast<char*>(h->d_hcd) + dvec);
   }
   r.err = reinterpret_cast<unsigned*>(base + off);
   for (int c0 = 0; c0 < n_cal; c0 += per_launch) {

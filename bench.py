@@ -718,6 +718,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: one-GPU rehearsal of the multi-rank run (every rank on device 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hist-pull", type=int, default=None,
+                    help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
@@ -732,6 +734,9 @@ def main():
         build.build(verbose=False)
     barrier(world)
     legs = set(args.legs.split(","))
+    if args.hist_pull is not None:
+        from aiyagari_hark_amd import _lib
+        _lib.handle(dev.index).set_options({_lib.AIY_OPT_HIST_PULL: args.hist_pull})
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]
     line = {

@@ -363,6 +363,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     2 .. 16) instead of a bisection step, and Brent runs in those
                                     coordinates; 2 (default): also a unit-slope step from a single
                                     point; 0: bisection bracketing, Brent in r */
+#define AIY_OPT_HIST_PULL 15       /* value != 0: the BiCGSTAB distribution solves of S <= 8 states
+                                    (the resident GE search and aiy_hist_solve) form every matvec by
+                                    PULLING each destination's lottery sources in ascending order
+                                    (hist_pull.h's inverse lottery) instead of LDS-atomic pushes:
+                                    deterministic run to run; 0: the push form.  S > 8 always pulls */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

@@ -134,3 +134,26 @@ def test_logsec_levels_same_roots(gpu):
         assert np.all(res.status == 0)
         assert np.max(np.abs(res.r - base.r)) <= 2e-7
     assert np.sum(out[2, True].bisection_steps) < np.sum(out[0, True].bisection_steps)
+
+
+def test_pull_matvec_sweep_deterministic(gpu):
+    """AIY_OPT_HIST_PULL: the distribution solves of the resident search pull each
+    destination's lottery sources in ascending order (no LDS atomics).  The same roots as
+    the push form within the search tolerance, and two sweeps bit-identical."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    h = _lib.handle(gpu.index)
+    cals = table2_calibrations()
+    kw = dict(n_a=3000, device=gpu, method="brent", resident=True)
+    prev = h.set_options({_lib.AIY_OPT_HIST_PULL: 0})
+    try:
+        push = solve_table2(cals, **kw)
+        h.set_options({_lib.AIY_OPT_HIST_PULL: 1})
+        a = solve_table2(cals, **kw)
+        b = solve_table2(cals, **kw)
+    finally:
+        h.set_options(prev)
+    print(f"\npull vs push max |dr| {np.max(np.abs(a.r - push.r)):.2e}; pull runs equal: {np.array_equal(a.r, b.r)}")
+    assert np.all(a.status == 0) and np.all(b.status == 0)
+    assert np.array_equal(a.r, b.r) and np.array_equal(a.K_supply, b.K_supply)
+    assert np.max(np.abs(a.r - push.r)) <= 2e-7

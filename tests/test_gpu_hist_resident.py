@@ -186,3 +186,28 @@ def test_pull_bicgstab_stress_size(gpu):
         print(f"\ncell {c}: {int(it[c])} matvecs, residual {res:.2e}, K {K[c]:.6f}")
         assert res < 1e-11, res
         assert abs(m[c].sum() - 1.0) < 1e-10
+
+
+@pytest.mark.parametrize("cluster", [0, 24])
+def test_pull_matvec_histogram_matches_push(gpu, cluster):
+    """AIY_OPT_HIST_PULL on the standalone BiCGSTAB solve of the 24 Table II cells (two
+    columns per thread at the default cluster, one at 24 workgroups): the same
+    distribution as the push form to the solve tolerance, and a repeat bit-identical."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import table2_calibrations
+    from oracle import stationary as ST
+    h = _lib.handle(gpu.index)
+    cals = table2_calibrations()
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 10000, 2)
+    r = np.linspace(0.02, 0.04, len(cals))
+    prev = h.set_options({_lib.AIY_OPT_HIST_PULL: 0})
+    try:
+        Kp, itp, mp, _ = _solve(gpu, cals, aGrid, r, True, cluster, accel=-1)
+        h.set_options({_lib.AIY_OPT_HIST_PULL: 1})
+        K1, it1, m1, _ = _solve(gpu, cals, aGrid, r, True, cluster, accel=-1)
+        K2, it2, m2, _ = _solve(gpu, cals, aGrid, r, True, cluster, accel=-1)
+    finally:
+        h.set_options(prev)
+    assert np.array_equal(m1, m2) and np.array_equal(it1, it2)
+    assert np.max(np.abs(m1 - mp)) < 1e-8
+    assert np.max(np.abs(K1 - Kp) / Kp) < 1e-5

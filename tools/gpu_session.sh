@@ -48,6 +48,9 @@ for step in "$@"; do
     trace_c3) export TMPDIR=/tmp; run trace_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c3 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs3 ;;
     pull) run pull 400 $PYT -s tests/test_gpu_hist_resident.py -k "pull or rouwenhorst" ;;
     c4) run c4 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pull7) run pull7 400 $PYT -s tests/test_gpu_hist_resident.py tests/test_gpu_ge_resident.py -k "pull" ;;
+    t2pull) run t2pull 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --hist-pull 1 ;;
+    t2push) run t2push 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --hist-pull 0 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
