@@ -890,6 +890,31 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 // force the solve's registers into scratch; the call costs a few register saves per
 // solve.  The span buffer / v share the caller's dynamic LDS.
 template <int SMAX, int KC, int TH, bool PULL = false>
+__device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io);
+// the same body inlined into the caller (the pull form spilled more as a separate function)
+template <int SMAX, int KC, int TH, bool PULL = false>
+__device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
+  extern __shared__ double hk_dyn_in[];
+  __shared__ int s_base[SMAX];
+  __shared__ int s_pub[2 * SMAX][2];
+  __shared__ int s_tot;
+  __shared__ HcCand s_cand[SMAX][kHcCand];
+  __shared__ int s_ncand[SMAX];
+  __shared__ unsigned short s_cinfo[PULL ? 1 : KC * SMAX * TH];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  __shared__ int s_ex[2 * SMAX];
+  const HkShared<SMAX, KC, TH> L{hk_dyn_in, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop, s_ex};
+  unsigned nb = *nb_io, ne = *ne_io;
+  const int mv = hk_solve<SMAX, KC, TH, PULL>(a, L, nb, ne);
+  *nb_io = nb;
+  *ne_io = ne;
+  return mv;
+}
+template <int SMAX, int KC, int TH, bool PULL>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn[];
   __shared__ int s_base[SMAX];

@@ -456,3 +456,26 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
 }
 
 }  // namespace aiy
+
+namespace aiy {
+
+// hp_solve with its LDS declared here (inlined into the caller: as a separate function it spilled
+// ~2.3 KB per lane, inlined into the device-resident GE search ~0.3 KB); the
+// staged inverse lottery shares the caller's dynamic LDS.
+template <int SMAX, int TH>
+__device__ __forceinline__ int hp_solve_lds(HpArgs a, unsigned* nb_io, unsigned* ne_io) {
+  extern __shared__ int hp_dyn_iso[];
+  __shared__ double s_P[SMAX * SMAX];
+  __shared__ int s_ex[2 * SMAX];
+  __shared__ double s_part[kHkRed][TH / kWave];
+  __shared__ double s_res[kHkRed];
+  __shared__ int s_flag, s_stop;
+  const HpShared<SMAX, TH> L{s_P, hp_dyn_iso, s_ex, s_part, s_res, &s_flag, &s_stop};
+  unsigned nb = *nb_io, ne = *ne_io;
+  const int mv = hp_solve<SMAX, TH>(a, L, nb, ne);
+  *nb_io = nb;
+  *ne_io = ne;
+  return mv;
+}
+
+}  // namespace aiy

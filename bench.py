@@ -509,14 +509,25 @@ def configs4_leg(args, world, rank, dev):
 
     solve()   # warm-up
     hist_stats(h, True, dev)
+    ge_stats(h, True, dev)
     barrier(world)
     t0 = time.perf_counter()
     res = solve()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     hist_ms, hist_n = hist_stats(h, True, dev)
-    pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
-    hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
+    ge_ms, ge_n, ge_pts, ge_cyc = ge_stats(h, True, dev)
+    if ge_n > 0:   # the device-resident search (ge_cluster_kernel<25, ...>, pull-form solves)
+        kern = ("ge_cluster_kernel<25, 0, 1, 512> (device-resident GE search: EGM cycles + lottery + pull-form "
+                "BiCGSTAB + root search)")
+        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * ge_pts + EGM_BYTES_PER_NODE_CYCLE * 25 * (n_a + 1) * ge_cyc
+        hist_ms, hist_n = ge_ms, ge_n
+        trace_name = "ge_cluster_kernel"
+    else:          # host-driven loop: the pull-form distribution solve is the dominant kernel
+        kern = "hist_pull_kernel<32, 512> (pull-form BiCGSTAB distribution solve, Krylov vectors in HBM)"
+        pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
+        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
+        trace_name = "hist_pull_kernel"
     gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[] if res is None else [float(x) for x in res.r],
                                    status=[] if res is None else [int(x) for x in res.status]), world)
@@ -527,9 +538,10 @@ def configs4_leg(args, world, rank, dev):
             r[k], st[k] = rr, ss
     out = dict(value=len(cells) / el, unit="GE solves/s", seconds=el, calibrations=len(cells), n_a=n_a, S=25,
                r_percent=[round(100 * x, 6) for x in r], status=st,
-               roofline={"kernel": "hist_bicg_kernel<25, 1, 512> (BiCGSTAB distribution solve, v in HBM)",
+               roofline={"kernel": kern,
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": gbs / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(trace_name + "_c4", scale=None),
                          "algorithmic_bytes_per_launch": hist_bytes / max(1, hist_n),
                          "avg_launch_ms": hist_ms / max(1, hist_n), "launches": hist_n,
                          "kernel_time_share": hist_ms * 1e-3 / max(1e-12, el)},

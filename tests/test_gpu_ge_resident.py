@@ -33,7 +33,10 @@ def test_resident_plan_shapes(gpu):
     assert p3 is not None and p3[0] >= G
     half = resident_plan(gpu, 24, 7, 10_000, cu_share=0.5)
     assert half is None or half[0] * 24 <= 128
-    assert resident_plan(gpu, 3, 25, 50_000) is None     # stress shape: the host loop
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    p25 = resident_plan(gpu, 3, 25, 50_000)              # configs[4]: every stress cell resident at once
+    assert p25 is not None and p25[0] * 3 <= cus and p25[2] == 1
+    assert resident_plan(gpu, 3, 16, 50_000) is None     # other S > 8: the host loop
     # clusters above 128 workgroups would escape the cluster reductions: the host loop runs
     assert resident_plan(gpu, 1, 7, 150_000) is None
     p1 = resident_plan(gpu, 1, 7, 120_000)
@@ -157,3 +160,18 @@ def test_pull_matvec_sweep_deterministic(gpu):
     assert np.all(a.status == 0) and np.all(b.status == 0)
     assert np.array_equal(a.r, b.r) and np.array_equal(a.K_supply, b.K_supply)
     assert np.max(np.abs(a.r - push.r)) <= 2e-7
+
+
+def test_resident_stress_matches_host_search(gpu):
+    """The 25-state resident search (register-accumulated EGM expectations, pull-form
+    distribution solves) against the host-driven loop on the stress cells at N_a = 6 000:
+    the same roots within the search tolerance."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst") for c in (1.0, 3.0, 5.0)]
+    kw = dict(n_a=6000, device=gpu, method="brent")
+    res = solve_table2(cals, resident=True, **kw)
+    ref = solve_table2(cals, resident=False, groups=1, **kw)
+    print(f"\nstress resident r {100 * res.r} host r {100 * ref.r}; evaluations {res.bisection_steps}")
+    assert np.all(res.status == 0) and np.all(ref.status == 0)
+    assert np.max(np.abs(res.r - ref.r)) <= 2e-7
+    assert np.max(np.abs(res.KtoY - ref.KtoY) / ref.KtoY) <= 2e-6
