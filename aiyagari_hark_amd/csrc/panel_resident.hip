@@ -107,7 +107,13 @@ __host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
   return ((size_t)n_cells * sizeof(CellHdr) + 15) / 16 * 16;
 }
 
-template <int TH, int NA, bool IN_LDS, bool QUAD>
+// FUSE (HBM-streaming form): the next period's labour draws ride in the lookup pass -- the
+// agent's labour state is already in a register there, so one streaming pass per period
+// reads (a, l) and writes (a', l') instead of a second pass over the labour states.  The two
+// lanes of an agent pair (consecutive agents, one Philox call per pair) split the pairs of
+// their NA agents and swap halves with one DPP exchange, so each lane still runs one
+// Philox call per two agents.
+template <int TH, int NA, bool IN_LDS, bool QUAD, bool FUSE = false>
 __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
   extern __shared__ __attribute__((aligned(16))) char s_dyn[];
   __shared__ double s_cdf[kLdsLab * kLdsLab];
@@ -224,6 +230,46 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
           local += an;
         }
       }
+      if constexpr (FUSE) {
+        if (p + 1 < r.n_periods) {   // period t + 1's labour from this period's (AS:1253-1254)
+          static_assert(NA % 2 == 0, "agent pairs split over the lane pair");
+          constexpr int H = NA / 2;
+          double u[NA];
+          const bool odd = (tid & 1) != 0;
+          if (r.u) {
+            const double* ut = r.u + (size_t)(t + 1 - r.t0) * r.u_ld + start;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+              const int i = base + k * TH + tid;
+              u[k] = i < cnt ? ut[i] : 0.0;
+            }
+          } else {
+            const unsigned ctr1 = (r.ge_iter << 20) | (unsigned)(t + 1);
+            double ue[H], uo[H];
+#pragma unroll
+            for (int h = 0; h < H; ++h) {   // even lane: pairs of its agents 0..H-1; odd lane: H..NA-1
+              const int k = odd ? h + H : h;
+              const long long i0 = r.offset + start + base + k * TH + (tid & ~1);
+#ifdef AIY_DIAG_NO_PHILOX
+              ue[h] = 0.37 + 1e-9 * (double)(i0 & 1023); uo[h] = 0.41 + 1e-9 * (double)(i0 & 1023);   // diagnostic
+#else
+              philox_uniform2(ctr1, (uint64_t)(i0 >> 1), r.seed, 0u, ue[h], uo[h]);
+#endif
+            }
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+              const double y = dpp_f64<kDppXor1>(odd ? ue[h] : uo[h]);   // the partner lane's half
+              u[h] = odd ? y : ue[h];
+              u[h + H] = odd ? uo[h] : y;
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < NA; ++k) {
+            const int i = base + k * TH + tid;
+            if (i < cnt) L[i] = (uint8_t)draw_labour(s_cdf, n_lab, ln[k], u[k]);
+          }
+        }
+      }
     }
 
     // ---- 2. publish the workgroup partial as two tagged granules ----
@@ -247,7 +293,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #ifndef AIY_DRAW_MODE
 #define AIY_DRAW_MODE 2
 #endif
-    if (p + 1 < r.n_periods) {
+    if (!FUSE && p + 1 < r.n_periods) {
 #if AIY_DRAW_MODE == 0   // every wave draws, wave 0 then sweeps
       draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid, TH);
 #elif AIY_DRAW_MODE == 1   // wave 4 takes wave 0's pairs
@@ -405,11 +451,17 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
        reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true>)},
       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false>),
        reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false>)}};
+  // streaming form with the labour draws fused into the lookup pass (AIY_OPT_RESIDENT_FUSE)
+  const void* fused[3] = {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true, true>),
+                          reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false, true, true>),
+                          reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false, true>)};
   static bool attr_set = false;
   if (!attr_set) {
     for (auto& row : kernels)
       for (const void* k : row)
         AIY_HIP(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
+    for (const void* k : fused)
+      AIY_HIP(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
     attr_set = true;
   }
   ResRun r;
@@ -422,7 +474,7 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   aiy_market mkc = mk;
   AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
-  const void* fn = kernels[sh.id][G.in_lds ? 1 : 0];
+  const void* fn = G.in_lds ? kernels[sh.id][1] : (h->res_fuse ? fused[sh.id] : kernels[sh.id][0]);
   // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
   // against the occupancy query; a plain launch then has the same residency as a
   // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),

@@ -368,6 +368,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     PULLING each destination's lottery sources in ascending order
                                     (hist_pull.h's inverse lottery) instead of LDS-atomic pushes:
                                     deterministic run to run; 0: the push form.  S > 8 always pulls */
+#define AIY_OPT_RESIDENT_FUSE 16   /* value != 0 (default): the HBM-streaming form of the resident panel
+                                    draws the next period's labour states inside the lookup pass (one
+                                    pass over the agents per period); 0: a separate draw pass */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

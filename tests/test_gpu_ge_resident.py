@@ -142,13 +142,15 @@ def test_logsec_levels_same_roots(gpu):
 def test_pull_matvec_sweep_deterministic(gpu):
     """AIY_OPT_HIST_PULL: the distribution solves of the resident search pull each
     destination's lottery sources in ascending order (no LDS atomics).  The same roots as
-    the push form within the search tolerance, and two sweeps bit-identical."""
+    the push form within the search tolerance, and -- in one launch (no rebalancing, whose
+    stop points follow the wall clock and change the cluster sizes, i.e. the summation order of
+    the cluster reductions) -- two sweeps bit-identical."""
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
     h = _lib.handle(gpu.index)
     cals = table2_calibrations()
     kw = dict(n_a=3000, device=gpu, method="brent", resident=True)
-    prev = h.set_options({_lib.AIY_OPT_HIST_PULL: 0})
+    prev = h.set_options({_lib.AIY_OPT_HIST_PULL: 0, _lib.AIY_OPT_GE_REBALANCE: 0})
     try:
         push = solve_table2(cals, **kw)
         h.set_options({_lib.AIY_OPT_HIST_PULL: 1})

@@ -48,6 +48,9 @@ def child(lib, opts):
         econ, agent = bench.make_economy(seed=0, n_agents=N, n_a=n_a, act_T=2000, device=dev, t_discard=500)
         econ.solve()
         bench_panel = agent.panel
+    fuse = int(os.environ.get("FUSE", "1"))
+    if hasattr(_lib, "AIY_OPT_RESIDENT_FUSE") and hasattr(h.lib, "aiy_get_option"):
+        h.set_options({_lib.AIY_OPT_RESIDENT_FUSE: fuse})
     for (res, agents, order, presort, Tt) in opts:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res), "opt")
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, order), "opt")
@@ -82,7 +85,8 @@ def child(lib, opts):
         h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), N, _lib.ptr(p.a), _lib.ptr(p.lab),
                                           3, 1, _lib.ptr(p.sow), Tt, ctypes.byref(ms),
                                           torch.cuda.current_stream().cuda_stream), "time")
-        out.append(dict(lib=os.path.basename(lib or "default"), resident=res, agents=agents, order=order, presort=presort, T=Tt,
+        out.append(dict(lib=os.path.basename(lib or "default"), fuse=fuse, resident=res, agents=agents, order=order,
+                        presort=presort, T=Tt,
                         us_per_period=1e3 * ms.value / Tt, K=float(p.a.mean())))
         print(json.dumps(out[-1]), flush=True)
 
