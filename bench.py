@@ -732,6 +732,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hist-pull", type=int, default=None,
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
+    ap.add_argument("--ge-rebalance", type=int, default=None,
+                    help="AIY_OPT_GE_REBALANCE for the resident searches (default: the library's)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
@@ -746,9 +748,14 @@ def main():
         build.build(verbose=False)
     barrier(world)
     legs = set(args.legs.split(","))
-    if args.hist_pull is not None:
+    if args.hist_pull is not None or args.ge_rebalance is not None:
         from aiyagari_hark_amd import _lib
-        _lib.handle(dev.index).set_options({_lib.AIY_OPT_HIST_PULL: args.hist_pull})
+        opts = {}
+        if args.hist_pull is not None:
+            opts[_lib.AIY_OPT_HIST_PULL] = args.hist_pull
+        if args.ge_rebalance is not None:
+            opts[_lib.AIY_OPT_GE_REBALANCE] = args.ge_rebalance
+        _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]
     line = {

@@ -54,6 +54,9 @@ for step in "$@"; do
     res25) run res25 400 $PYT -s tests/test_gpu_ge_resident.py -k "stress or plan_shapes" ;;
     panelfuse3) run panelfuse3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,1,0,200],[1,0,2,0,200]]' FUSE=1 python -u tools/panel_variants.py ;;
     panelnofuse3) run panelnofuse3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,1,0,200],[1,0,2,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
+    t2q34) run t2q34 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 34 ;;
+    t2q67) run t2q67 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 67 ;;
+    t2q25) run t2q25 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 25 ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
