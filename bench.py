@@ -237,8 +237,11 @@ def table2_leg(args, world, rank, dev):
                hist_gbs=hist_gbs, hist_bytes_per_launch=hist_bytes / max(1, hist_n), s8d_gbs=s8d_gbs,
                s8d_bytes_per_launch=s8d_bytes / max(1, hist_n),
                hist_avg_launch_ms=hist_ms / max(1, hist_n),
-               evaluations_rank0=per_rank[0]["evaluations"], r_percent=[round(100 * x, 6) for x in r],
-               saving_rate_percent=[round(100 * 0.08 * x, 5) for x in kty])
+               evaluations_rank0=per_rank[0]["evaluations"], r_percent=[round(100 * x, 5) for x in r],
+               saving_rate_percent=[round(100 * 0.08 * x, 4) for x in kty],
+               r_note="r_percent rounded to the root search's tolerance (r_tol = 1e-7: 1e-5 percentage points); "
+                      "digits below it follow the rebalancing stop points, which follow the wall clock "
+                      "(DESIGN.md §4e); with AIY_OPT_GE_REBALANCE = 0 a sweep is bit-reproducible")
     log(f"[bench] table2: {el / args.steps:.3f} s per sweep ({out['value']:.2f} GE solves/s); "
         f"hist kernel {hist_ms / args.steps:.1f} ms per sweep, {hist_gbs:.0f} GB/s algorithmic; "
         f"hist_point_iters={point_iters} hist_launches={hist_n}")
@@ -537,7 +540,7 @@ def configs4_leg(args, world, rank, dev):
         for k, rr, ss in zip(pr["cells"], pr["r"], pr["status"]):
             r[k], st[k] = rr, ss
     out = dict(value=len(cells) / el, unit="GE solves/s", seconds=el, calibrations=len(cells), n_a=n_a, S=25,
-               r_percent=[round(100 * x, 6) for x in r], status=st,
+               r_percent=[round(100 * x, 5) for x in r], status=st,
                roofline={"kernel": kern,
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS,
@@ -811,7 +814,7 @@ def main():
                                           "note": "algorithmic bytes of all launches of a sweep / sweep wall time"}},
         "table2": {k: t2[k] for k in ("seconds_per_sweep", "evaluations_rank0", "hist_launches_per_sweep",
                                       "hist_kernel_ms_per_sweep", "resident", "egm_cycles_per_sweep", "r_percent",
-                                      "saving_rate_percent")},
+                                      "saving_rate_percent", "r_note")},
         "cpu_baseline": None,
     }
     if args.dist_backend == "gloo" and world > 1:

@@ -231,8 +231,9 @@ def test_bench_two_rank_rehearsal_matches_one_rank(gpu):
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert "rehearsal" in two
     # the per-calibration searches do not depend on the split (same cluster size per cell);
-    # r_percent is rounded to 1e-6 percentage points
-    assert np.max(np.abs(np.array(two["table2"]["r_percent"]) - one["table2"]["r_percent"])) <= 2e-6
+    # r_percent is rounded to the search tolerance (1e-5 percentage points); two ranks run other
+    # rebalancing launches than one (another summation order): equal within that tolerance
+    assert np.max(np.abs(np.array(two["table2"]["r_percent"]) - one["table2"]["r_percent"])) <= 1.0001e-5
     k1, k2 = np.array(one["configs3"]["K_first"]), np.array(two["configs3"]["K_first"])
     assert np.max(np.abs(k1 - k2) / k1) < 1e-12
     assert abs(one["configs3"]["K_final"] - two["configs3"]["K_final"]) / one["configs3"]["K_final"] < 1e-12
@@ -254,7 +255,7 @@ def test_bench_eight_rank_rehearsal_matches_one_rank(gpu):
     # (r_tol = 1e-7, i.e. 1e-5 percentage points)
     dr = np.max(np.abs(np.array(eight["table2"]["r_percent"]) - one["table2"]["r_percent"]))
     print(f"\n8-rank rehearsal: max |dr| = {dr:.2e} pp")
-    assert dr <= 1e-5
+    assert dr <= 1.0001e-5
     k1, k8 = np.array(one["configs3"]["K_first"]), np.array(eight["configs3"]["K_first"])
     assert np.max(np.abs(k1 - k8) / k1) < 1e-12
     assert abs(one["configs3"]["K_final"] - eight["configs3"]["K_final"]) / one["configs3"]["K_final"] < 1e-12
