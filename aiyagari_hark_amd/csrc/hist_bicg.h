@@ -155,16 +155,27 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   if constexpr (PULL) {
     const int n1 = n_a + 1;
     unsigned bad = 0u;
+    // a lottery written in this launch (the resident GE search): every workgroup's entries are
+    // in memory before the neighbour's column j0 - 1 is read
+    if (r.lottery_fresh) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!barrier()) return -1;
+    }
     for (int q = tid; q < S * n_own; q += TH) {
       const int s = q / n_own, j = j0 + (q - s * n_own);
       const int l = lo_at(s, j);
       const int lp = j > 0 ? lo_at(s, j - 1) : -1;
-      if (l < lp || l < 0 || l > n_a - 2) bad = 2u;
-      const int dhi = l < lp ? lp : l;
-      for (int d = lp + 1; d <= dhi; ++d)
+      // only a monotone lottery inside the grid is scattered (anything else: error 2, the
+      // caller falls back); the loops never index outside the row
+      const bool ok = l >= 0 && l <= n_a - 2 && lp >= -1 && lp <= l;
+      if (!ok) {
+        bad = 2u;
+        continue;
+      }
+      for (int d = lp + 1; d <= l; ++d)
         __hip_atomic_store(to_global(&Ainv[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (j == n_a - 1)
-        for (int d = dhi + 1; d <= n_a; ++d)
+        for (int d = l + 1; d <= n_a; ++d)
           __hip_atomic_store(to_global(&Ainv[(size_t)s * n1 + d]), n_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (S * aspan * (int)sizeof(int) > cap * (int)sizeof(double)) bad = 2u;
@@ -509,9 +520,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         for (int u = 0; u < GRP; ++u) {
           const int sc = min(s0 + u, S - 1);
           const int* As = s_A + sc * aspan - (j0 - 1);
-          a0[u] = valid ? As[d - 1] : 0;
-          a1[u] = valid ? As[d] : 0;
-          a2[u] = valid ? As[d + 1] : 0;
+          // (clamped into the row: the loops below never leave it)
+          a0[u] = valid ? min(max(As[d - 1], 0), n_a) : 0;
+          a1[u] = valid ? min(max(As[d], a0[u]), n_a) : 0;
+          a2[u] = valid ? min(max(As[d + 1], a1[u]), n_a) : 0;
           const int i0 = min(a1[u], n_a - 1), i1 = min(a1[u] + 1, n_a - 1);
           const int i2 = min(a0[u], n_a - 1), i3 = min(a0[u] + 1, n_a - 1);
           wv[u][0] = w_at(sc, i0); qv[u][0] = q_at(sc, i0);

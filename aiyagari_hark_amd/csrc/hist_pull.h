@@ -112,16 +112,24 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     s_P[q] = (s < S && sp < S) ? ((const double*)r.Pc)[s * S + sp] : 0.0;
   }
   unsigned bad = 0u;
+  // a lottery written in this launch (the resident GE search): every workgroup's entries are
+  // in memory before the neighbour's column j0 - 1 is read
+  if (r.lottery_fresh && !barrier()) return -1;
   for (int q = tid; q < S * n_own; q += TH) {
     const int s = q / n_own, j = j0 + (q - s * n_own);
     const int l = lo_at(s, j);
     const int lp = j > 0 ? lo_at(s, j - 1) : -1;
-    if (l < lp || l < 0 || l > n_a - 2) bad = 2u;
-    const int dhi = l < lp ? lp : l;
-    for (int d = lp + 1; d <= dhi; ++d) __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
+    // only a monotone lottery inside the grid is scattered (anything else: error 2, the caller
+    // falls back); the loops never index outside the row
+    const bool ok = l >= 0 && l <= n_a - 2 && lp >= -1 && lp <= l;
+    if (!ok) {
+      bad = 2u;
+      continue;
+    }
+    for (int d = lp + 1; d <= l; ++d)
+      __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (j == n_a - 1)
-      for (int d = dhi + 1; d <= n_a; ++d)
+      for (int d = l + 1; d <= n_a; ++d)
         __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), n_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -186,9 +194,10 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     for (int u = 0; u < GRP; ++u) {
       const int s = s0 + u < S ? s0 + u : S - 1;
       const int* As = s_A + s * span - (j0 - 1);
-      a0[u] = valid ? As[d - 1] : 0;
-      a1[u] = valid ? As[d] : 0;
-      a2[u] = valid ? As[d + 1] : 0;
+      // (clamped into the row: the loops below never leave it)
+      a0[u] = valid ? min(max(As[d - 1], 0), n_a) : 0;
+      a1[u] = valid ? min(max(As[d], a0[u]), n_a) : 0;
+      a2[u] = valid ? min(max(As[d + 1], a1[u]), n_a) : 0;
       const int i0 = min(a1[u], n_a - 1), i1 = min(a1[u] + 1, n_a - 1);
       const int i2 = min(a0[u], n_a - 1), i3 = min(a0[u] + 1, n_a - 1);
       wv[u][0] = w_at(s, i0); qv[u][0] = q_at(Q, s, i0);

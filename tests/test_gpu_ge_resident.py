@@ -139,7 +139,8 @@ def test_logsec_levels_same_roots(gpu):
     assert np.sum(out[2, True].bisection_steps) < np.sum(out[0, True].bisection_steps)
 
 
-def test_pull_matvec_sweep_deterministic(gpu):
+@pytest.mark.parametrize("n_a", [3000, 10000])   # one and two columns per thread at 24 cells
+def test_pull_matvec_sweep_deterministic(gpu, n_a):
     """AIY_OPT_HIST_PULL: the distribution solves of the resident search pull each
     destination's lottery sources in ascending order (no LDS atomics).  The same roots as
     the push form within the search tolerance, and -- in one launch (no rebalancing, whose
@@ -149,7 +150,7 @@ def test_pull_matvec_sweep_deterministic(gpu):
     from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
     h = _lib.handle(gpu.index)
     cals = table2_calibrations()
-    kw = dict(n_a=3000, device=gpu, method="brent", resident=True)
+    kw = dict(n_a=n_a, device=gpu, method="brent", resident=True)
     prev = h.set_options({_lib.AIY_OPT_HIST_PULL: 0, _lib.AIY_OPT_GE_REBALANCE: 0})
     try:
         push = solve_table2(cals, **kw)
