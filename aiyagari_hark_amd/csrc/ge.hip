@@ -138,7 +138,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   std::vector<double> etol(n_cal, o->egm_tol), htol(n_cal, o->hist_tol);
   std::vector<char> loose(n_cal, 0), refine(n_cal, 0);
   const bool loose_on = o->loose_bracket && o->method == 1;
-  const double kLooseEgm = std::max(o->egm_tol, AIY_GE_LOOSE_EGM), kLooseHist = std::max(o->hist_tol, AIY_GE_LOOSE_HIST);
+  const double kLooseEgm = std::max(o->egm_tol, AIY_GE_LOOSE_EGM), kLooseHist = std::max(o->hist_tol, std::pow(10.0, -(double)h->ge_loose_hist));
   const unsigned sec_blocks = 1024;
   AIY_HIP(h, hipMemsetAsync(Mg, 0, sizeof(double) * n_cal, st));
 

@@ -77,6 +77,7 @@ struct GeRun {
   int extrap_period;      // EGM cycles between extrapolation checks (>= 4)
   int logsec;             // log-secant bracketing (AIY_OPT_GE_LOGSEC, with loose bracketing)
   int pull;               // distribution solves by the lottery pull (AIY_OPT_HIST_PULL): deterministic
+  double loose_hist;      // loose-bracketing histogram tolerance (AIY_OPT_GE_LOOSE_HIST)
   double* qb;             // [n_cal][S][n_a] pull form: the matvec input rows
   double* vec4;           // [n_cal][4][S][n_a] S > 8: the pull form's Krylov vectors (r, p, v, t)
   int* ainv;              // [n_cal][S][n_a + 1] pull form: inverse lottery
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
         st.Kd = KtoL;
         st.loose = g.loose && g.method == 1 && !st.rs.brent && !st.rs.done && !st.refine;
         st.etol = st.loose ? fmax(g.egm_tol, AIY_GE_LOOSE_EGM) : g.egm_tol;
-        st.htol = st.loose ? fmax(g.hist_tol, AIY_GE_LOOSE_HIST) : g.hist_tol;
+        st.htol = st.loose ? fmax(g.hist_tol, g.loose_hist) : g.hist_tol;
         st.warm_egm = g.warm_egm && st.steps > 0;
         st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
         st.fresh_mass = !(g.warm_hist && st.steps > 0);
@@ -1078,6 +1079,7 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.ainv = reinterpret_cast<int*>(base + L.ainv);
   g.vec4 = reinterpret_cast<double*>(base + L.vec4);
   g.pull = h->hist_pull;
+  g.loose_hist = std::pow(10.0, -(double)h->ge_loose_hist);
   g.lo = reinterpret_cast<int*>(base + L.lo);
   g.wlo = reinterpret_cast<double*>(base + L.wlo);
   g.slab = reinterpret_cast<double*>(base + L.slab);

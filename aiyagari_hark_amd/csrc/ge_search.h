@@ -150,9 +150,7 @@ struct RootSearch {
 #ifndef AIY_GE_LOOSE_EGM
 #define AIY_GE_LOOSE_EGM 1e-6
 #endif
-#ifndef AIY_GE_LOOSE_HIST
-#define AIY_GE_LOOSE_HIST 1e-10
-#endif
+// (the histogram's loose tolerance is the handle option AIY_OPT_GE_LOOSE_HIST, default 1e-10)
 constexpr double kGeSignMargin = 0.05;
 
 }  // namespace aiy

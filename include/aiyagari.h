@@ -371,6 +371,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 #define AIY_OPT_RESIDENT_FUSE 16   /* value != 0 (default): the HBM-streaming form of the resident panel
                                     draws the next period's labour states inside the lookup pass (one
                                     pass over the agents per period); 0: a separate draw pass */
+#define AIY_OPT_GE_LOOSE_HIST 17   /* value v in [6, 14] (default 10): the loose-bracketing evaluations'
+                                    distribution tolerance is 10^-v (their sign needs |K_s - K_d| >= 5 %
+                                    of K_d; the final bracket's evaluations use the full tolerance) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);
