@@ -135,6 +135,55 @@ def test_rccl_path_one_rank_equals_unsharded(gpu):
     _check(got, ref)
 
 
+def _torch_comm_rank(port, q, N, T, seed):
+    """One rank of a torch.distributed RCCL ("nccl") group: the library borrows torch's own
+    communicator (parallel.bind_rccl -> aiy_comm_bind) and runs the sharded-path panel."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from aiyagari_hark_amd import _lib
+        from aiyagari_hark_amd.parallel import bind_rccl, unbind_rccl
+        h = _lib.handle(0)
+        world, rank, kind = bind_rccl(h)
+        try:
+            fx = _fixture()
+            lab0 = np.random.default_rng(8).integers(0, 7, N)
+            p = _panel(dev, fx, N, T)
+            _reset(p, fx, lab0)
+            p.run(0, T, shock_mode="philox", seed=seed, ge_iter=1)
+            torch.cuda.synchronize()
+            q.put((kind, p.lab.cpu().numpy(), p.a.cpu().numpy(), p.hist_A.cpu().numpy(), p.hist_M.cpu().numpy()))
+        finally:
+            unbind_rccl(h)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_torch_communicator_bound_equals_unsharded(gpu):
+    """bind_rccl borrows torch.distributed's RCCL communicator (one communicator per device:
+    torch's bundled librccl is the only RCCL in the process); with one rank the library's
+    RCCL period path gives the unsharded history."""
+    import multiprocessing as mp
+    fx = _fixture()
+    N, T, seed = 150_003, 30, 21
+    lab0 = np.random.default_rng(8).integers(0, 7, N)
+    ref = _unsharded(gpu, fx, N, T, lab0, seed)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    proc = ctx.Process(target=_torch_comm_rank, args=(_free_port(), q, N, T, seed))
+    proc.start()
+    kind, *got = q.get(timeout=240)
+    proc.join(timeout=60)
+    assert proc.exitcode == 0
+    assert kind == "torch"
+    _check(tuple(got), ref)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
