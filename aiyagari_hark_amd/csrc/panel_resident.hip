@@ -440,8 +440,23 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
                         int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
   if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
-  const ResShape sh = res_shape(h);
-  const ResGeometry G = res_geometry(h, n, P.tab.g.n_cells, sh);
+  ResShape sh = res_shape(h);
+  ResGeometry G = res_geometry(h, n, P.tab.g.n_cells, sh);
+  if (!G.in_lds && h->res_shape_stream >= 0 && h->res_shape_stream != sh.id) {
+    // the HBM-streaming form has its own shape (default 1024 x 4: 4 waves per SIMD hide the
+    // streamed agents' latency better, 1 150 vs 1 504 us per period at 1e8 agents,
+    // profiles/r05h_panel_shapes.jsonl)
+    ResShape ss = sh;
+    const int keep = h->res_shape;
+    h->res_shape = h->res_shape_stream;
+    ss = res_shape(h);
+    h->res_shape = keep;
+    const ResGeometry Gs = res_geometry(h, n, P.tab.g.n_cells, ss);
+    if (!Gs.in_lds) {
+      sh = ss;
+      G = Gs;
+    }
+  }
   int32_t rc = ensure_res_scratch(h);
   if (rc) return rc;
   const void* kernels[3][2] = {

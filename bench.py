@@ -507,8 +507,11 @@ def configs4_leg(args, world, rank, dev):
 
     share = cu_share(world)
 
+    resident = None if args.c4_resident < 0 else bool(args.c4_resident)
+
     def solve():
-        return solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share) if cals else None
+        return (solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share, resident=resident)
+                if cals else None)
 
     solve()   # warm-up
     hist_stats(h, True, dev)
@@ -737,6 +740,8 @@ def main():
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     ap.add_argument("--ge-rebalance", type=int, default=None,
                     help="AIY_OPT_GE_REBALANCE for the resident searches (default: the library's)")
+    ap.add_argument("--c4-resident", type=int, default=-1,
+                    help="configs4: 1 the device-resident search, 0 the host-driven loop, -1 the default")
     ap.add_argument("--ge-loose-hist", type=int, default=None,
                     help="AIY_OPT_GE_LOOSE_HIST (loose-bracketing histogram tolerance 10^-v; default the library's)")
     args = ap.parse_args()

@@ -368,12 +368,16 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     PULLING each destination's lottery sources in ascending order
                                     (hist_pull.h's inverse lottery) instead of LDS-atomic pushes:
                                     deterministic run to run; 0: the push form.  S > 8 always pulls */
-#define AIY_OPT_RESIDENT_FUSE 16   /* value != 0 (default): the HBM-streaming form of the resident panel
-                                    draws the next period's labour states inside the lookup pass (one
-                                    pass over the agents per period); 0: a separate draw pass */
-#define AIY_OPT_GE_LOOSE_HIST 17   /* value v in [6, 14] (default 10): the loose-bracketing evaluations'
+#define AIY_OPT_RESIDENT_FUSE 16   /* value != 0: the HBM-streaming form of the resident panel draws the
+                                    next period's labour states inside the lookup pass (one pass over
+                                    the agents per period); 0 (default): a separate draw pass (faster
+                                    with the default streaming shape) */
+#define AIY_OPT_GE_LOOSE_HIST 17   /* value v in [6, 14] (default 8): the loose-bracketing evaluations'
                                     distribution tolerance is 10^-v (their sign needs |K_s - K_d| >= 5 %
                                     of K_d; the final bracket's evaluations use the full tolerance) */
+#define AIY_OPT_RESIDENT_SHAPE_STREAM 18 /* workgroup shape (AIY_OPT_RESIDENT_SHAPE's values) of the resident
+                                    panel's HBM-streaming form (agents beyond LDS, e.g. configs[3]);
+                                    default 1 (1024 threads x 4 agents); -1: AIY_OPT_RESIDENT_SHAPE */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

@@ -31,11 +31,19 @@ def main():
     ap.add_argument("--rebalance", type=int, default=-1, help="AIY_OPT_GE_REBALANCE (-1: default)")
     ap.add_argument("--extrap", type=int, default=-1, help="AIY_OPT_GE_EXTRAP_PERIOD (-1: default)")
     ap.add_argument("--logsec", type=int, default=-1, help="AIY_OPT_GE_LOGSEC (-1: default)")
+    ap.add_argument("--loose-hist", type=int, default=-1, help="AIY_OPT_GE_LOOSE_HIST (-1: default)")
+    ap.add_argument("--stress", action="store_true", help="configs[4]'s 3 cells (25 states) instead of Table II")
     args = ap.parse_args()
     from aiyagari_hark_amd import _lib
-    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2, table2_calibrations
     dev = torch.device("cuda:0")
-    cals = table2_calibrations()[:args.cells]
+    if args.stress:
+        cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst")
+                for c in (1.0, 3.0, 5.0)]
+        if args.n_a == 10_000:
+            args.n_a = 50_000
+    else:
+        cals = table2_calibrations()[:args.cells]
     h = _lib.handle(0)
     if args.cluster_cap:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_HIST_CLUSTER, args.cluster_cap), "opt")
@@ -43,11 +51,13 @@ def main():
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, args.rebalance), "opt")
     if args.logsec >= 0:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOGSEC, args.logsec), "opt")
+    if args.loose_hist >= 0:
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_LOOSE_HIST, args.loose_hist), "opt")
     if args.extrap >= 0:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_EXTRAP_PERIOD, args.extrap), "opt")
     out = {}
     for mode in args.modes.split(","):
-        kw = dict(n_a=args.n_a, device=dev, method="brent", resident=mode == "resident")
+        kw = dict(n_a=args.n_a, device=dev, method="brent", resident=mode == "resident", groups=1)
         solve_table2(cals, **kw)
         torch.cuda.synchronize()
         ts = []
@@ -81,7 +91,7 @@ def main():
             out["evaluations"] = [[dict(r=float(x[0]), f_rel=float(x[1]), egm_cycles=int(x[2]), matvecs=int(x[3]),
                                         loose=int(x[4]), us=round(float(x[5]), 1)) for x in e[c] if x[2] > 0]
                                   for c in range(ne)]
-            for c in (0, 11, 23):
+            for c in ((0, 1, 2) if args.stress else (0, 11, 23)):
                 if c < ne:
                     print(f"[evals] cell {c}: " + "; ".join(f"r={x['r']:.6f} f={x['f_rel']:+.1e} cyc={x['egm_cycles']} "
                                                             f"mv={x['matvecs']}{' L' if x['loose'] else ''}"

@@ -59,6 +59,11 @@ for step in "$@"; do
     t2q25) run t2q25 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 25 ;;
     t2lh8) run t2lh8 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 8 ;;
     t2lh9) run t2lh9 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 9 ;;
+    c4host) run c4host 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --c4-resident 0 ;;
+    c4res) run c4res 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --c4-resident 1 ;;
+    profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
+    t2lh7) run t2lh7 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 7 ;;
+    panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;

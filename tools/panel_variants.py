@@ -51,6 +51,8 @@ def child(lib, opts):
     fuse = int(os.environ.get("FUSE", "1"))
     if hasattr(_lib, "AIY_OPT_RESIDENT_FUSE") and hasattr(h.lib, "aiy_get_option"):
         h.set_options({_lib.AIY_OPT_RESIDENT_FUSE: fuse})
+    if hasattr(_lib, "AIY_OPT_RESIDENT_SHAPE_STREAM") and hasattr(h.lib, "aiy_get_option"):
+        h.set_options({_lib.AIY_OPT_RESIDENT_SHAPE_STREAM: -1})   # the shape under test for both forms
     for (res, agents, order, presort, Tt) in opts:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res), "opt")
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, order), "opt")
