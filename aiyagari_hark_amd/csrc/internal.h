@@ -44,8 +44,8 @@ struct aiy_handle {
   int hist_krylov = 0;               // AIY_OPT_HIST_KRYLOV: resident histogram solves by BiCGSTAB
   int res_fuse = 0;                  // AIY_OPT_RESIDENT_FUSE: streaming panel draws fused into the lookup pass
   int res_shape_stream = 1;          // AIY_OPT_RESIDENT_SHAPE_STREAM: shape of the HBM-streaming form (-1: res_shape)
-  int hist_pull = 0;
-  int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
+  int hist_pull = 0;                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
+  int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value
   // per-calibration tolerances for one call (aiy_ge_stationary's loose bracketing); null: the
   // scalar tolerance of the call.  Device arrays [n_cal]; egm_tolh: the host copy.
   const double* egm_tolv = nullptr;
