@@ -928,6 +928,9 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
   if (S > 8) {   // configs[4]'s 25 states: the pull-form solve, every cluster as large as the device allows
+    // (opt-in: inlined into the search kernel the 25-state pull solve runs at ~270 us per matvec
+    // against ~100 us as its own kernel, so the host-driven loop is faster: 11.0 vs 8.3 GE solves/s)
+    if (!h->ge_resident_wide) return false;
     p.th = 512;
     p.kc = 1;
     p.smax = kGeSmax;

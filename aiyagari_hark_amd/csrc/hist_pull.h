@@ -346,6 +346,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   auto rh_at = [&](int s, int j) { return hk_rhat((unsigned)(s * n_a + j) + seed * 0x5BD1E995u); };
   double best = __builtin_inf();
   int mv_best = 0;
+  double rm_cur = 0.0;   // this thread's part of max|r| of the current r (kept from where r was written)
+  double alpha = 0.0;
   while (true) {
     if (restart) {
       // t = T x, r = t - x (p = r); the converged answer is t
@@ -368,6 +370,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       part[2] = xs;
       if (!reduce(part, 3, 2u)) return -1;
       rho = L.s_res[0];
+      rm_cur = rm;
       if (mv == 1) total0 = L.s_res[2];
       if (L.s_res[1] < tol || mv >= r.max_iter) {
         const double scale = total0 / L.s_res[2];
@@ -382,18 +385,17 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
       s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
     // v = p - T p; alpha = rho / <rh, v>; max|r| rides along
-    double rvv = 0.0, rm = 0.0;
+    double rvv = 0.0;
     if (!matvec(Pv, [&](int s, int j, double out) {
           const size_t g = (size_t)s * n_a + j;
           const double v = Pv[g] - out;
           Vv[g] = v;
           rvv += rh_at(s, j) * v;
-          rm = nan_max(rm, fabs(Rv[g]));
         }))
       return -1;
     ++mv;
     part[0] = rvv;
-    part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
+    part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm_cur;
     if (!reduce(part, 2, 2u)) return -1;
     if (L.s_res[1] >= kHkStopSentinel) return -(2 + mv);
     if ((!first && L.s_res[1] < tol) || mv >= r.max_iter) {
@@ -410,16 +412,13 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       continue;
     }
     first = false;
-    const double alpha = rho / L.s_res[0];
+    alpha = rho / L.s_res[0];
     if (!(fabs(alpha) < 1e300)) {
       restart = true;
       continue;
     }
-    // s = r - alpha v (into R); x += alpha p
-    own_points([&](int s, int j, size_t g) {
-      put(Rv, s, j, Rv[g] - alpha * Vv[g]);
-      put(X, s, j, X[g] + alpha * Pv[g]);
-    });
+    // s = r - alpha v (into R); x += alpha p waits for the omega step (one pass over x)
+    own_points([&](int s, int j, size_t g) { put(Rv, s, j, Rv[g] - alpha * Vv[g]); });
     // t = s - T s; omega = <t, s> / <t, t>
     double ts = 0.0, tt = 0.0, rs = 0.0, rt = 0.0, sm = 0.0;
     if (!matvec(Rv, [&](int s, int j, double out) {
@@ -444,21 +443,26 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     if (!reduce(part, 5, 16u)) return -1;
     double omega = (L.s_res[4] < tol) ? 0.0 : L.s_res[0] / L.s_res[1];
     if (!(fabs(omega) < 1e300)) omega = 0.0;
-    if (omega == 0.0) {
+    if (omega == 0.0) {   // x + alpha p is the answer (or <t, t> = 0): verify
+      own_points([&](int s, int j, size_t g) { put(X, s, j, X[g] + alpha * Pv[g]); });
       restart = true;
       continue;
     }
     const double rho2 = L.s_res[2] - omega * L.s_res[3];
     const double beta = (rho2 / rho) * (alpha / omega);
     rho = rho2;
-    // x += omega s; r = s - omega t; p = r + beta (p - omega v)
+    // x += alpha p + omega s (the p of this step, before its update); r = s - omega t;
+    // p = r + beta (p - omega v); max|r| for the next step's check
+    double rmn = 0.0;
     own_points([&](int s, int j, size_t g) {
-      const double sv = Rv[g], t = Tv[g];
-      put(X, s, j, X[g] + omega * sv);
+      const double sv = Rv[g], t = Tv[g], pold = Pv[g];
+      put(X, s, j, (X[g] + alpha * pold) + omega * sv);
       const double rn = sv - omega * t;
       put(Rv, s, j, rn);
-      put(Pv, s, j, rn + beta * (Pv[g] - omega * Vv[g]));
+      put(Pv, s, j, rn + beta * (pold - omega * Vv[g]));
+      rmn = nan_max(rmn, fabs(rn));
     });
+    rm_cur = rmn;
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }
   return mv;

@@ -45,6 +45,7 @@ struct aiy_handle {
   int res_fuse = 0;                  // AIY_OPT_RESIDENT_FUSE: streaming panel draws fused into the lookup pass
   int res_shape_stream = 1;          // AIY_OPT_RESIDENT_SHAPE_STREAM: shape of the HBM-streaming form (-1: res_shape)
   int hist_pull = 0;                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
+  bool ge_resident_wide = false;     // AIY_OPT_GE_RESIDENT_WIDE: the 25-state shape on the resident search too
   int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value
   // per-calibration tolerances for one call (aiy_ge_stationary's loose bracketing); null: the
   // scalar tolerance of the call.  Device arrays [n_cal]; egm_tolh: the host copy.

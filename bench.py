@@ -508,6 +508,8 @@ def configs4_leg(args, world, rank, dev):
     share = cu_share(world)
 
     resident = None if args.c4_resident < 0 else bool(args.c4_resident)
+    if resident:   # the 25-state shape on the resident search is opt-in (AIY_OPT_GE_RESIDENT_WIDE)
+        h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
 
     def solve():
         return (solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share, resident=resident)

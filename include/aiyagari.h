@@ -378,6 +378,9 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 #define AIY_OPT_RESIDENT_SHAPE_STREAM 18 /* workgroup shape (AIY_OPT_RESIDENT_SHAPE's values) of the resident
                                     panel's HBM-streaming form (agents beyond LDS, e.g. configs[3]);
                                     default 1 (1024 threads x 4 agents); -1: AIY_OPT_RESIDENT_SHAPE */
+#define AIY_OPT_GE_RESIDENT_WIDE 19 /* value != 0: the device-resident search also takes the 25-state shape
+                                    (configs[4]; pull-form solves inlined into the search kernel); 0
+                                    (default): that shape runs the host-driven loop, which is faster */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

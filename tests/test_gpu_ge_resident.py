@@ -34,9 +34,16 @@ def test_resident_plan_shapes(gpu):
     half = resident_plan(gpu, 24, 7, 10_000, cu_share=0.5)
     assert half is None or half[0] * 24 <= 128
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
-    p25 = resident_plan(gpu, 3, 25, 50_000)              # configs[4]: every stress cell resident at once
-    assert p25 is not None and p25[0] * 3 <= cus and p25[2] == 1
-    assert resident_plan(gpu, 3, 16, 50_000) is None     # other S > 8: the host loop
+    from aiyagari_hark_amd import _lib
+    h = _lib.handle(gpu.index)
+    assert resident_plan(gpu, 3, 25, 50_000) is None     # configs[4] by default: the host loop (faster)
+    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
+    try:
+        p25 = resident_plan(gpu, 3, 25, 50_000)          # opt-in: every stress cell resident at once
+        assert p25 is not None and p25[0] * 3 <= cus and p25[2] == 1
+        assert resident_plan(gpu, 3, 16, 50_000) is None  # other S > 8: the host loop
+    finally:
+        h.set_options(prev)
     # clusters above 128 workgroups would escape the cluster reductions: the host loop runs
     assert resident_plan(gpu, 1, 7, 150_000) is None
     p1 = resident_plan(gpu, 1, 7, 120_000)
@@ -171,8 +178,14 @@ def test_resident_stress_matches_host_search(gpu):
     the same roots within the search tolerance."""
     from aiyagari_hark_amd.stationary import Calibration, solve_table2
     cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst") for c in (1.0, 3.0, 5.0)]
+    from aiyagari_hark_amd import _lib
+    h = _lib.handle(gpu.index)
     kw = dict(n_a=6000, device=gpu, method="brent")
-    res = solve_table2(cals, resident=True, **kw)
+    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
+    try:
+        res = solve_table2(cals, resident=True, **kw)
+    finally:
+        h.set_options(prev)
     ref = solve_table2(cals, resident=False, groups=1, **kw)
     print(f"\nstress resident r {100 * res.r} host r {100 * ref.r}; evaluations {res.bisection_steps}")
     assert np.all(res.status == 0) and np.all(ref.status == 0)
