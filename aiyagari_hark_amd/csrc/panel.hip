@@ -297,7 +297,8 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
 
   // the persistent kernel simulates the employed sub-states only (Krusell-Smith mode runs
   // the per-period kernel)
-  if (!h->comm && h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P)) {
+  if (!h->comm && h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P) &&
+      resident_aligned(a, lab)) {
     // one persistent launch for the whole block of periods (panel_resident.hip)
     hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
     rc = launch_resident(h, P, mk, n_local, a, lab, u, u_ld, seed, ge_iter, t0, n_periods, sow, hist_A, hist_M, st);
@@ -421,7 +422,8 @@ extern "C" int32_t aiy_sim_kernel_time(aiy_handle* h, const aiy_panel_model* mod
   const int nb = sim_blocks(n_local);
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, 0);
   AIY_CHECK_LAUNCH(h);
-  if (h->use_resident && n_local >= kResMinAgents && resident_supported(P)) {
+  if (h->use_resident && n_local >= kResMinAgents && resident_supported(P) &&
+      resident_aligned(a, lab)) {
     // one persistent launch of n_launch periods
     rc = time_launches(h, st, 1,
                        [&] {

@@ -353,6 +353,10 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
                         int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st);
 int32_t resident_status(aiy_handle* h, hipStream_t st);
 bool resident_supported(const PanelDev& P);
+// the persistent kernel moves agent pairs as 16-byte asset / 2-byte labour accesses
+inline bool resident_aligned(const double* a, const uint8_t* lab) {
+  return (reinterpret_cast<uintptr_t>(a) & 15) == 0 && (reinterpret_cast<uintptr_t>(lab) & 1) == 0;
+}
 constexpr long long kResMinAgents = 65536;
 
 }  // namespace aiy

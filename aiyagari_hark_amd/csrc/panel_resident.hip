@@ -78,6 +78,19 @@ __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long lon
   const int nthr = nvt;
   for (int q0 = vt; 2 * q0 < cnt; q0 += G * nthr) {
     double u0[G], u1[G];
+    int l0[G], l1[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {   // the pair's labour states first (one 2-byte load), in flight across Philox
+      const int i = 2 * (q0 + g * nthr);
+      if (i + 1 < cnt) {
+        const unsigned v = *reinterpret_cast<const unsigned short*>(L + i);
+        l0[g] = (int)(v & 0xffu);
+        l1[g] = (int)(v >> 8);
+      } else {
+        l0[g] = i < cnt ? L[i] : 0;
+        l1[g] = 0;
+      }
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int i = 2 * (q0 + g * nthr);
@@ -95,8 +108,13 @@ __device__ __forceinline__ void draw_slice(const ResRun& r, uint8_t* L, long lon
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int i = 2 * (q0 + g * nthr);
-      if (i < cnt) L[i] = (uint8_t)draw_labour(s_cdf, n_lab, L[i], u0[g]);
-      if (i + 1 < cnt) L[i + 1] = (uint8_t)draw_labour(s_cdf, n_lab, L[i + 1], u1[g]);
+      const int n0 = draw_labour(s_cdf, n_lab, l0[g], u0[g]);
+      if (i + 1 < cnt) {
+        const int n1 = draw_labour(s_cdf, n_lab, l1[g], u1[g]);
+        *reinterpret_cast<unsigned short*>(L + i) = (unsigned short)(n0 | (n1 << 8));
+      } else if (i < cnt) {
+        L[i] = (uint8_t)n0;
+      }
     }
   }
 }
@@ -183,9 +201,36 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 
     // ---- 1. agents: lookups, a = m - c, partial sum ----
     double local = 0.0;
+    constexpr bool kPairs = !IN_LDS && !FUSE && NA % 2 == 0;
     for (int base = 0; base < cnt; base += TH * NA) {
       double m[NA];
       int ln[NA], cell[NA];
+      // agent of slot k: consecutive lanes take consecutive agents (i = base + k TH + tid), except
+      // the unfused streaming form: agent PAIRS per lane (i = base + 2 (k/2 TH + tid) + k%2), so the
+      // assets move as 16-byte loads / stores and the labour states as 2-byte ones
+      if constexpr (kPairs) {
+#pragma unroll
+        for (int kp = 0; kp < NA / 2; ++kp) {
+          const int i = base + 2 * (kp * TH + tid);
+          double a0, a1;
+          int q0, q1;
+          if (i + 1 < cnt) {
+            const double2 av = *reinterpret_cast<const double2*>(A + i);
+            const unsigned lv = *reinterpret_cast<const unsigned short*>(L + i);
+            a0 = av.x; a1 = av.y; q0 = (int)(lv & 0xffu); q1 = (int)(lv >> 8);
+          } else {   // tail lanes: dummy work on the last agent
+            const int ic = i < cnt ? i : cnt - 1;
+            a0 = a1 = A[ic];
+            q0 = q1 = L[ic];
+          }
+          ln[2 * kp] = q0;
+          ln[2 * kp + 1] = q1;
+          m[2 * kp] = Rnow * a0 + Wnow * (s_lvl[q0] * 1.0);                              // AS:1283
+          m[2 * kp + 1] = Rnow * a1 + Wnow * (s_lvl[q1] * 1.0);
+          cell[2 * kp] = (2 * q0 + Mrkv) * n_J + jc;                                     // employed (Urate = 0)
+          cell[2 * kp + 1] = (2 * q1 + Mrkv) * n_J + jc;
+        }
+      } else
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
         const int i0 = base + k * TH + tid;
@@ -217,6 +262,21 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
         atomicAdd(&s_wdiag[tid / kWave], (unsigned long long)(w1 - w0));
       }
 #endif
+      if constexpr (kPairs) {
+#pragma unroll
+        for (int kp = 0; kp < NA / 2; ++kp) {
+          const int i = base + 2 * (kp * TH + tid);
+          const double an0 = m[2 * kp] - c[2 * kp], an1 = m[2 * kp + 1] - c[2 * kp + 1];   // AS:1415
+          if (i + 1 < cnt) {
+            *reinterpret_cast<double2*>(A + i) = make_double2(an0, an1);
+            local += an0;
+            local += an1;
+          } else if (i < cnt) {
+            A[i] = an0;
+            local += an0;
+          }
+        }
+      } else
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
         const int i = base + k * TH + tid;
@@ -440,6 +500,8 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
                         int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
   if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
+  if (!resident_aligned(a, lab))
+    return fail(h, AIY_ERR_ARG, "resident panel: assets must be 16-byte and labour states 2-byte aligned");
   ResShape sh = res_shape(h);
   ResGeometry G = res_geometry(h, n, P.tab.g.n_cells, sh);
   if (!G.in_lds && h->res_shape_stream >= 0 && h->res_shape_stream != sh.id) {

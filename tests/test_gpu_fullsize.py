@@ -132,7 +132,7 @@ def test_streaming_resident_kernel_1M_agents(big, solved, gpu):
     h = _lib.handle(gpu.index)
     out = {}
     try:
-        for name, resident, stream in (("stream", 1, 1), ("period", 0, 0), ("lds", 1, 0)):
+        for name, resident, stream in (("stream", 1, 1), ("period", 0, 0), ("lds", 1, 0), ("stream2", 1, 1)):
             h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, resident), "opt")
             h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_STREAM, stream), "opt")
             p = _panel(gpu, m, md, cd, solved["batch"], T)
@@ -150,5 +150,8 @@ def test_streaming_resident_kernel_1M_agents(big, solved, gpu):
         assert np.max(np.abs(a - ref[1])) / np.max(np.abs(ref[1])) < 1e-12, name
         assert np.max(np.abs(hA - ref[2]) / ref[2]) < 1e-12, name
         assert np.max(np.abs(hM - ref[3]) / ref[3]) < 1e-12, name
-    # the two persistent forms sum the workgroup partials in the same fixed order
-    assert np.array_equal(out["stream"][2], out["lds"][2])
+    # the streaming form has its own shape and agent-pair lanes (AIY_OPT_RESIDENT_SHAPE_STREAM),
+    # so its partial sums group differently from the LDS form's; each is reproducible run to run
+    assert np.max(np.abs(out["stream"][2] - out["lds"][2]) / out["lds"][2]) < 1e-13
+    for k in range(4):
+        assert np.array_equal(out["stream"][k], out["stream2"][k])

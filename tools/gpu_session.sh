@@ -64,7 +64,10 @@ for step in "$@"; do
     profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
     t2lh7) run t2lh7 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 7 ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
+    panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
+    panelshapes1) run panelshapes1 400 env NAG=1000006 T=400 OPTS='[[1,0,0,0,400],[1,0,1,0,400],[1,0,2,0,400]]' FUSE=0 python -u tools/panel_variants.py ;;
     nlab) run nlab 400 $PYT tests/test_gpu_nlab.py ;;
+    fullsize) run fullsize 500 $PYT tests/test_gpu_fullsize.py ;;
     benchsize) run benchsize 500 $PYT tests/test_gpu_benchsize.py ;;
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
     suite) run suite 1000 $PYT -m gpu tests ;;
