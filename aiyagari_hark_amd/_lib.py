@@ -45,6 +45,7 @@ AIY_OPT_RESIDENT_FUSE = 16
 AIY_OPT_GE_LOOSE_HIST = 17
 AIY_OPT_RESIDENT_SHAPE_STREAM = 18
 AIY_OPT_GE_RESIDENT_WIDE = 19
+AIY_OPT_RESIDENT_ENGINE = 20
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

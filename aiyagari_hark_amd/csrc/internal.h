@@ -44,6 +44,7 @@ struct aiy_handle {
   int hist_krylov = 0;               // AIY_OPT_HIST_KRYLOV: resident histogram solves by BiCGSTAB
   int res_fuse = 0;                  // AIY_OPT_RESIDENT_FUSE: streaming panel draws fused into the lookup pass
   int res_shape_stream = 1;          // AIY_OPT_RESIDENT_SHAPE_STREAM: shape of the HBM-streaming form (-1: res_shape)
+  int res_engine = 0;                // AIY_OPT_RESIDENT_ENGINE: streaming form by the loader ring (sim_stream_kernel)
   int hist_pull = 0;                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
   bool ge_resident_wide = false;     // AIY_OPT_GE_RESIDENT_WIDE: the 25-state shape on the resident search too
   int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value

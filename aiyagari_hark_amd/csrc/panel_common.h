@@ -51,8 +51,11 @@ __host__ __device__ inline PanelTabGeom panel_tab_geom(int n_lab, int n_M, int n
   g.Z = 2 * n_a;
   g.n_J = n_M > 1 ? n_M - 1 : 1;
   g.n_cells = (unemployed ? 4 : 2) * n_lab * g.n_J;
+#ifndef AIY_TAB_LG_MAX
+#define AIY_TAB_LG_MAX 13
+#endif
   int lg = 4;                                  // ~n_a buckets per octave (~Z / 2), 16 .. 8192
-  while (lg < 13 && (1 << lg) < n_a) ++lg;
+  while (lg < AIY_TAB_LG_MAX && (1 << lg) < n_a) ++lg;
   g.shift = 52 - lg;
   g.buckets = kTabOctaves << lg;
   g.rec_stride = 4LL * (g.Z + 1);

@@ -381,6 +381,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
 #define AIY_OPT_GE_RESIDENT_WIDE 19 /* value != 0: the device-resident search also takes the 25-state shape
                                     (configs[4]; pull-form solves inlined into the search kernel); 0
                                     (default): that shape runs the host-driven loop, which is faster */
+#define AIY_OPT_RESIDENT_ENGINE 20 /* value != 0: the resident panel's HBM-streaming form runs as a loader
+                                    ring (4 loader waves stream the agents through LDS, 12 consumer
+                                    waves look up; slower at configs[3]: 1 420 vs 1 002 us per period);
+                                    0 (default): every wave streams its own agents
+                                    (AIY_OPT_RESIDENT_SHAPE_STREAM) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

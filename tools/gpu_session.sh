@@ -63,6 +63,10 @@ for step in "$@"; do
     c4res) run c4res 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --c4-resident 1 ;;
     profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
     t2lh7) run t2lh7 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 7 ;;
+    lgnt) for e in 1 0; do run lgnt$e 500 env ENGINE=$e NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=lg11=aiyagari_hark_amd/lib/variants/libaiyagari_lg11.so,lg12=aiyagari_hark_amd/lib/variants/libaiyagari_lg12.so,nt=aiyagari_hark_amd/lib/variants/libaiyagari_nt.so python -u tools/panel_variants.py; done ;;
+    sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
+    sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
+    ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panelshapes1) run panelshapes1 400 env NAG=1000006 T=400 OPTS='[[1,0,0,0,400],[1,0,1,0,400],[1,0,2,0,400]]' FUSE=0 python -u tools/panel_variants.py ;;

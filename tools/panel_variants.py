@@ -53,6 +53,8 @@ def child(lib, opts):
         h.set_options({_lib.AIY_OPT_RESIDENT_FUSE: fuse})
     if hasattr(_lib, "AIY_OPT_RESIDENT_SHAPE_STREAM") and hasattr(h.lib, "aiy_get_option"):
         h.set_options({_lib.AIY_OPT_RESIDENT_SHAPE_STREAM: -1})   # the shape under test for both forms
+    if hasattr(_lib, "AIY_OPT_RESIDENT_ENGINE") and hasattr(h.lib, "aiy_get_option"):
+        h.set_options({_lib.AIY_OPT_RESIDENT_ENGINE: int(os.environ.get("ENGINE", "1"))})
     for (res, agents, order, presort, Tt) in opts:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT, res), "opt")
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_RESIDENT_SHAPE, order), "opt")
@@ -78,7 +80,15 @@ def child(lib, opts):
         p.run(0, T, shock_mode="philox", seed=1)
         torch.cuda.synchronize()
         if presort:   # global wealth order (Philox keyed by position: timing experiment only)
-            key, perm = torch.sort(p.a)
+            # PRESORT_KEY=la: by (labour state, assets); default: by assets
+            pk = os.environ.get("PRESORT_KEY", "")
+            k = p.a + 1e4 * p.lab.double() if pk in ("la", "local") else p.a
+            if pk == "local":   # within each workgroup's slice of the streaming form (256 slices)
+                ch = (N + 255) // 256
+                ch += ch & 1
+                k = k + 1e6 * (torch.arange(N, device=dev) // ch).double()
+            key, perm = torch.sort(k)
+            key = p.a[perm]
             p.a.copy_(key)
             p.lab.copy_(p.lab[perm])
             torch.cuda.synchronize()
@@ -87,7 +97,7 @@ def child(lib, opts):
         h.check(h.lib.aiy_sim_kernel_time(h.h, ctypes.byref(pm), ctypes.byref(mk), N, _lib.ptr(p.a), _lib.ptr(p.lab),
                                           3, 1, _lib.ptr(p.sow), Tt, ctypes.byref(ms),
                                           torch.cuda.current_stream().cuda_stream), "time")
-        out.append(dict(lib=os.path.basename(lib or "default"), fuse=fuse, resident=res, agents=agents, order=order,
+        out.append(dict(lib=os.path.basename(lib or "default"), fuse=fuse, engine=os.environ.get("ENGINE", "1"), resident=res, agents=agents, order=order,
                         presort=presort, T=Tt,
                         us_per_period=1e3 * ms.value / Tt, K=float(p.a.mean())))
         print(json.dumps(out[-1]), flush=True)
