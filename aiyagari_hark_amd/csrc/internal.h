@@ -47,6 +47,7 @@ struct aiy_handle {
   int res_engine = 0;                // AIY_OPT_RESIDENT_ENGINE: streaming form by the loader ring (sim_stream_kernel)
   int hist_pull = 0;                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
   bool ge_resident_wide = false;     // AIY_OPT_GE_RESIDENT_WIDE: the 25-state shape on the resident search too
+  bool ge_loose_brent = false;       // AIY_OPT_GE_LOOSE_BRENT: host-driven search, Brent's evaluations loose too
   int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value
   // per-calibration tolerances for one call (aiy_ge_stationary's loose bracketing); null: the
   // scalar tolerance of the call.  Device arrays [n_cal]; egm_tolh: the host copy.

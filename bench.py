@@ -746,6 +746,8 @@ def main():
                     help="configs4: 1 the device-resident search, 0 the host-driven loop, -1 the default")
     ap.add_argument("--ge-loose-hist", type=int, default=None,
                     help="AIY_OPT_GE_LOOSE_HIST (loose-bracketing histogram tolerance 10^-v; default the library's)")
+    ap.add_argument("--ge-loose-brent", type=int, default=None,
+                    help="AIY_OPT_GE_LOOSE_BRENT (host-driven search: Brent's evaluations loose too)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
@@ -760,7 +762,8 @@ def main():
         build.build(verbose=False)
     barrier(world)
     legs = set(args.legs.split(","))
-    if args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None:
+    if (args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None or
+            args.ge_loose_brent is not None):
         from aiyagari_hark_amd import _lib
         opts = {}
         if args.hist_pull is not None:
@@ -769,6 +772,8 @@ def main():
             opts[_lib.AIY_OPT_GE_REBALANCE] = args.ge_rebalance
         if args.ge_loose_hist is not None:
             opts[_lib.AIY_OPT_GE_LOOSE_HIST] = args.ge_loose_hist
+        if args.ge_loose_brent is not None:
+            opts[_lib.AIY_OPT_GE_LOOSE_BRENT] = args.ge_loose_brent
         _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]

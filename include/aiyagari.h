@@ -386,6 +386,10 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     waves look up; slower at configs[3]: 1 420 vs 1 002 us per period);
                                     0 (default): every wave streams its own agents
                                     (AIY_OPT_RESIDENT_SHAPE_STREAM) */
+#define AIY_OPT_GE_LOOSE_BRENT 21  /* value != 0: the host-driven search (aiy_ge_stationary without the
+                                    device-resident search) also runs Brent's evaluations at the loose
+                                    tolerances, refining any whose |K_s - K_d| is below the sign
+                                    margin; 0 (default): loose during bracketing only */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

@@ -66,6 +66,7 @@ for step in "$@"; do
     lgnt) for e in 1 0; do run lgnt$e 500 env ENGINE=$e NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=lg11=aiyagari_hark_amd/lib/variants/libaiyagari_lg11.so,lg12=aiyagari_hark_amd/lib/variants/libaiyagari_lg12.so,nt=aiyagari_hark_amd/lib/variants/libaiyagari_nt.so python -u tools/panel_variants.py; done ;;
     sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
+    c4lb) run c4lb0 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline && run c4lb1 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline --ge-loose-brent 1 ;;
     ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
