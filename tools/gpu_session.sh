@@ -67,6 +67,9 @@ for step in "$@"; do
     sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     c4lb) run c4lb0 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline && run c4lb1 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline --ge-loose-brent 1 ;;
+    sub8) run sub8_32 400 python -u tools/table2_rank_subsets.py 8 32 && run sub8_85 400 python -u tools/table2_rank_subsets.py 8 85 ;;
+    sub8b) run sub8_16 400 python -u tools/table2_rank_subsets.py 8 16 && run sub8_24 400 python -u tools/table2_rank_subsets.py 8 24 && run sub8_48 400 python -u tools/table2_rank_subsets.py 8 48 ;;
+    g3) run g3 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0 ;;
     ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
