@@ -32,6 +32,7 @@
 namespace aiy {
 
 constexpr int kHpHeavy = 64;   // sources of one destination above which its wave sums them
+constexpr int kHpUnroll = 4;   // wave strides of a heavy sum with their loads in flight together
 
 struct HpArgs {
   int G, S, n_a, w, j0, j1;
@@ -208,7 +209,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
 #pragma unroll
     for (int u = 0; u < GRP; ++u) {
       const int s = s0 + u;
-      if (s >= S) break;   // wave-uniform
+      if (s >= S) continue;   // wave-uniform (continue, not break: the loop stays fully unrolled)
       const int n1c = a2[u] - a1[u], n0c = a1[u] - a0[u];
       const bool heavy = valid && (n1c + n0c) > kHpHeavy;
       double acc = 0.0;
@@ -226,9 +227,32 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         hm &= hm - 1ull;
         const int b0 = __builtin_amdgcn_readlane(a0[u], h), b1 = __builtin_amdgcn_readlane(a1[u], h),
                   b2 = __builtin_amdgcn_readlane(a2[u], h);
+        // lane-strided partials, kHpUnroll strides' loads in flight at once (the same order)
         double pa = 0.0, pb = 0.0;
-        for (int j = b1 + lane; j < b2; j += kWave) pa += w_at(s, j) * q_at(Q, s, j);
-        for (int j = b0 + lane; j < b1; j += kWave) pb += (1.0 - w_at(s, j)) * q_at(Q, s, j);
+        for (int j = b1 + lane; j < b2; j += kHpUnroll * kWave) {
+          double wj[kHpUnroll], qj[kHpUnroll];
+#pragma unroll
+          for (int e = 0; e < kHpUnroll; ++e) {
+            const int jc = min(j + e * kWave, b2 - 1);
+            wj[e] = w_at(s, jc);
+            qj[e] = q_at(Q, s, jc);
+          }
+#pragma unroll
+          for (int e = 0; e < kHpUnroll; ++e)
+            if (j + e * kWave < b2) pa += wj[e] * qj[e];
+        }
+        for (int j = b0 + lane; j < b1; j += kHpUnroll * kWave) {
+          double wj[kHpUnroll], qj[kHpUnroll];
+#pragma unroll
+          for (int e = 0; e < kHpUnroll; ++e) {
+            const int jc = min(j + e * kWave, b1 - 1);
+            wj[e] = w_at(s, jc);
+            qj[e] = q_at(Q, s, jc);
+          }
+#pragma unroll
+          for (int e = 0; e < kHpUnroll; ++e)
+            if (j + e * kWave < b1) pb += (1.0 - wj[e]) * qj[e];
+        }
         const double ta = wave_sum_lane63(pa), tb = wave_sum_lane63(pb);
         const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
         if (lane == h) acc = tot;
@@ -250,13 +274,26 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         if (s0 < S) pull_group(Q, s0, d, valid, Tq);
       }
       if (valid) {
+        // the own values Q[sp][d] the fused updates need, a chunk of states at a time, loaded
+        // together ahead of the chunk's stores (a load after a store to another vector is not
+        // hoisted past it: one load round trip per state otherwise)
+        constexpr int CH = 8;
 #pragma unroll
-        for (int sp = 0; sp < SMAX; ++sp) {
-          if (sp < S) {
-            double acc = 0.0;
+        for (int sp0 = 0; sp0 < SMAX; sp0 += CH) {
+          if (sp0 < S) {   // wave-uniform
+            double qo[CH];
 #pragma unroll
-            for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * Tq[s];   // (P.T @ T)[sp, d]
-            fuse(sp, d, acc);
+            for (int u = 0; u < CH; ++u) qo[u] = sp0 + u < S ? Q[(size_t)(sp0 + u) * n_a + d] : 0.0;
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int sp = sp0 + u;
+              if (sp < S) {
+                double acc = 0.0;
+#pragma unroll
+                for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * Tq[s];   // (P.T @ T)[sp, d]
+                fuse(sp, d, acc, qo[u]);
+              }
+            }
           }
         }
       }
@@ -329,10 +366,28 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     return s_flag != 0;
   };
   // every own point once (elementwise updates between the matvecs)
-  auto own_points = [&](auto&& f) {
-    for (int q = tid; q < S * n_own; q += TH) {
-      const int s = q / n_own, j = j0 + (q - s * n_own);
-      f(s, j, (size_t)s * n_a + j);
+  // every own point once (elementwise updates between the matvecs), UP points per thread at a
+  // time: ld(g) -> the point's inputs for all UP points first, then st(s, j, g, inputs) (the
+  // next points' loads are not hoisted past this point's stores otherwise)
+  auto own_points = [&](auto&& ld, auto&& st) {
+    constexpr int UP = 4;
+    const int np = S * n_own;
+    for (int q0 = tid; q0 < np; q0 += UP * TH) {
+      decltype(ld((size_t)0)) in[UP];
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        const int q = min(q0 + u * TH, np - 1);
+        const int s = q / n_own, j = j0 + (q - s * n_own);
+        in[u] = ld((size_t)s * n_a + j);
+      }
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        const int q = q0 + u * TH;
+        if (q < np) {
+          const int s = q / n_own, j = j0 + (q - s * n_own);
+          st(s, j, (size_t)s * n_a + j, in[u]);
+        }
+      }
     }
   };
 
@@ -352,9 +407,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     if (restart) {
       // t = T x, r = t - x (p = r); the converged answer is t
       double rr = 0.0, rm = 0.0, xs = 0.0;
-      if (!matvec(X, [&](int s, int j, double out) {
+      if (!matvec(X, [&](int s, int j, double out, double x) {
             const size_t g = (size_t)s * n_a + j;
-            const double x = X[g];
             const double rv = out - x;
             Tv[g] = out;
             put(Rv, s, j, rv);
@@ -375,7 +429,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       if (L.s_res[1] < tol || mv >= r.max_iter) {
         const double scale = total0 / L.s_res[2];
         const bool one = mv == 1;
-        own_points([&](int s, int j, size_t g) { put(X, s, j, one ? Tv[g] : Tv[g] * scale); });
+        own_points([&](size_t g) { return Tv[g]; },
+                   [&](int s, int j, size_t, double t) { put(X, s, j, one ? t : t * scale); });
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         break;
       }
@@ -386,9 +441,9 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
     // v = p - T p; alpha = rho / <rh, v>; max|r| rides along
     double rvv = 0.0;
-    if (!matvec(Pv, [&](int s, int j, double out) {
+    if (!matvec(Pv, [&](int s, int j, double out, double pq) {
           const size_t g = (size_t)s * n_a + j;
-          const double v = Pv[g] - out;
+          const double v = pq - out;
           Vv[g] = v;
           rvv += rh_at(s, j) * v;
         }))
@@ -418,12 +473,11 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       continue;
     }
     // s = r - alpha v (into R); x += alpha p waits for the omega step (one pass over x)
-    own_points([&](int s, int j, size_t g) { put(Rv, s, j, Rv[g] - alpha * Vv[g]); });
+    own_points([&](size_t g) { return Rv[g] - alpha * Vv[g]; }, [&](int s, int j, size_t, double v) { put(Rv, s, j, v); });
     // t = s - T s; omega = <t, s> / <t, t>
     double ts = 0.0, tt = 0.0, rs = 0.0, rt = 0.0, sm = 0.0;
-    if (!matvec(Rv, [&](int s, int j, double out) {
+    if (!matvec(Rv, [&](int s, int j, double out, double sv) {
           const size_t g = (size_t)s * n_a + j;
-          const double sv = Rv[g];
           const double t = sv - out;
           Tv[g] = t;
           const double h = rh_at(s, j);
@@ -444,7 +498,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     double omega = (L.s_res[4] < tol) ? 0.0 : L.s_res[0] / L.s_res[1];
     if (!(fabs(omega) < 1e300)) omega = 0.0;
     if (omega == 0.0) {   // x + alpha p is the answer (or <t, t> = 0): verify
-      own_points([&](int s, int j, size_t g) { put(X, s, j, X[g] + alpha * Pv[g]); });
+      own_points([&](size_t g) { return X[g] + alpha * Pv[g]; }, [&](int s, int j, size_t, double v) { put(X, s, j, v); });
       restart = true;
       continue;
     }
@@ -454,14 +508,17 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     // x += alpha p + omega s (the p of this step, before its update); r = s - omega t;
     // p = r + beta (p - omega v); max|r| for the next step's check
     double rmn = 0.0;
-    own_points([&](int s, int j, size_t g) {
-      const double sv = Rv[g], t = Tv[g], pold = Pv[g];
-      put(X, s, j, (X[g] + alpha * pold) + omega * sv);
-      const double rn = sv - omega * t;
-      put(Rv, s, j, rn);
-      put(Pv, s, j, rn + beta * (pold - omega * Vv[g]));
-      rmn = nan_max(rmn, fabs(rn));
-    });
+    struct Up2 {
+      double sv, t, pold, x, v;
+    };
+    own_points([&](size_t g) { return Up2{Rv[g], Tv[g], Pv[g], X[g], Vv[g]}; },
+               [&](int s, int j, size_t, const Up2& u) {
+                 put(X, s, j, (u.x + alpha * u.pold) + omega * u.sv);
+                 const double rn = u.sv - omega * u.t;
+                 put(Rv, s, j, rn);
+                 put(Pv, s, j, rn + beta * (u.pold - omega * u.v));
+                 rmn = nan_max(rmn, fabs(rn));
+               });
     rm_cur = rmn;
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }

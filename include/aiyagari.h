@@ -390,6 +390,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     device-resident search) also runs Brent's evaluations at the loose
                                     tolerances, refining any whose |K_s - K_d| is below the sign
                                     margin; 0 (default): loose during bracketing only */
+#define AIY_OPT_HIST_ONCHIP 22     /* value != 0: distribution solves with S > 8 states run one calibration
+                                    per launch on every CU with the BiCGSTAB vectors on chip (registers
+                                    + LDS) when a workgroup's share fits (slower at configs[4]: its
+                                    256-workgroup barriers and reductions); 0 (default): all
+                                    calibrations at once, vectors in HBM (the pull form) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);

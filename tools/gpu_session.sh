@@ -70,6 +70,8 @@ for step in "$@"; do
     sub8) run sub8_32 400 python -u tools/table2_rank_subsets.py 8 32 && run sub8_85 400 python -u tools/table2_rank_subsets.py 8 85 ;;
     sub8b) run sub8_16 400 python -u tools/table2_rank_subsets.py 8 16 && run sub8_24 400 python -u tools/table2_rank_subsets.py 8 24 && run sub8_48 400 python -u tools/table2_rank_subsets.py 8 48 ;;
     g3) run g3 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0 ;;
+    onchip) run onchip 500 $PYT tests/test_gpu_benchsize.py::test_stress_ge_matches_oracle_fullsize tests/test_gpu_benchsize.py::test_stress_capital_supply_at_oracle_root tests/test_gpu_parity.py::test_rouwenhorst_25_state_histogram ;;
+    occheck) run occheck 300 python -u tools/onchip_check.py 50000 ;;
     ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
