@@ -96,6 +96,23 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   // column passes: every lane of a wave takes part in every pass (the heavy sums need the
   // whole wave), lanes past the own columns carry valid = false
   const int npass = (n_own + TH - 1) / TH;
+#ifdef AIY_DIAG_PHASES
+  // diagnostic build: 100 MHz ticks per phase -- 0 pull + mix + fuse, 1 matvec barrier,
+  // 2 reductions, 3 elementwise updates, 4 setup
+  unsigned long long hph[5] = {0, 0, 0, 0, 0}, htq = __builtin_amdgcn_s_memrealtime();
+#define HP_PH(k)                                                          \
+  do {                                                                    \
+    if (tid == 0) {                                                       \
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();     \
+      hph[(k)] += tn - htq;                                               \
+      htq = tn;                                                           \
+    }                                                                     \
+  } while (0)
+#else
+#define HP_PH(k) \
+  do {           \
+  } while (0)
+#endif
 
   auto barrier = [&]() -> bool {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores have left
@@ -262,7 +279,9 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   };
   // out = T Q on every own point, handed to fuse(s', d, out) in column order
   auto matvec = [&](const double* Q, auto&& fuse) -> bool {
+    HP_PH(3);
     if (!barrier()) return false;   // every workgroup's Q is in memory
+    HP_PH(1);
     for (int k = 0; k < npass; ++k) {
       const int d = j0 + tid + k * TH;
       const bool valid = d < j1;
@@ -298,10 +317,12 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         }
       }
     }
+    HP_PH(0);
     return true;
   };
   // cluster-wide reduction (hist_bicg.h's protocol: tagged granules, fixed order)
   auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax) -> bool {
+    HP_PH(3);
 #pragma unroll
     for (int v = 0; v < kHkRed; ++v) {
       if (v < nv) {
@@ -363,6 +384,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       }
     }
     __syncthreads();
+    HP_PH(2);
     return s_flag != 0;
   };
   // every own point once (elementwise updates between the matvecs)
@@ -403,6 +425,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   int mv_best = 0;
   double rm_cur = 0.0;   // this thread's part of max|r| of the current r (kept from where r was written)
   double alpha = 0.0;
+  HP_PH(4);
   while (true) {
     if (restart) {
       // t = T x, r = t - x (p = r); the converged answer is t
@@ -522,6 +545,13 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     rm_cur = rmn;
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }
+#ifdef AIY_DIAG_PHASES
+  if (tid == 0 && (w == 0 || w == G / 2 || w == G - 1) && mv > 0)
+    printf("[pull phases] wg %d/%d cols %d npass %d matvecs %d us/matvec: pull+mix %.2f barrier %.2f reduce %.2f "
+           "updates %.2f (setup %.1f us)\n", w, G, n_own, npass, mv, hph[0] * 0.01 / mv, hph[1] * 0.01 / mv,
+           hph[2] * 0.01 / mv, hph[3] * 0.01 / mv, hph[4] * 0.01);
+#endif
+#undef HP_PH
   return mv;
 }
 
