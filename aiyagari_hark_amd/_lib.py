@@ -41,13 +41,8 @@ AIY_OPT_GE_REBALANCE = 12
 AIY_OPT_GE_EXTRAP_PERIOD = 13
 AIY_OPT_GE_LOGSEC = 14
 AIY_OPT_HIST_PULL = 15
-AIY_OPT_RESIDENT_FUSE = 16
 AIY_OPT_GE_LOOSE_HIST = 17
 AIY_OPT_RESIDENT_SHAPE_STREAM = 18
-AIY_OPT_GE_RESIDENT_WIDE = 19
-AIY_OPT_RESIDENT_ENGINE = 20
-AIY_OPT_GE_LOOSE_BRENT = 21
-AIY_OPT_HIST_ONCHIP = 22
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

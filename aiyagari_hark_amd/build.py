@@ -19,7 +19,7 @@ LIB = os.path.join(LIBDIR, "libaiyagari.so")
 SOURCES = ["api.hip", "index.hip", "egm.hip", "panel_tab.hip", "panel.hip", "panel_block.hip", "panel_resident.hip",
            "hist.hip", "hist_resident.hip", "hist_krylov.hip", "stats.hip", "ge.hip", "ge_resident.hip", "hooks.hip"]
 HEADERS = ["common.h", "internal.h", "panel_common.h", "hist_cluster.h", "egm_common.h", "hist_bicg.h", "ge_search.h",
-           "hist_pull.h", "hist_onchip.h"]
+           "hist_pull.h"]
 ARCH = os.environ.get("AIY_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics", "-Wall", "-Wno-unused-result",
           "-I/opt/rocm/include"]

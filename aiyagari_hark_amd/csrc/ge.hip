@@ -178,9 +178,8 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     AIY_CHECK_LAUNCH(h);
     if (loose_on) {
       for (int c = 0; c < n_cal; ++c) {
-        // bracketing evaluations run loose; with AIY_OPT_GE_LOOSE_BRENT Brent's too (their f feeds
-        // the interpolation only while |f| >= the sign margin, else the point is refined)
-        loose[c] = (!rs[c].brent || h->ge_loose_brent) && !rs[c].done && !refine[c];
+        // bracketing evaluations run loose (Brent's at the full tolerances)
+        loose[c] = !rs[c].brent && !rs[c].done && !refine[c];
         etol[c] = loose[c] ? kLooseEgm : o->egm_tol;
         htol[c] = loose[c] ? kLooseHist : o->hist_tol;
       }

@@ -36,7 +36,6 @@
 #include "ge_search.h"
 #include "hist_bicg.h"
 #include "hist_cluster.h"
-#include "hist_pull.h"
 #include "internal.h"
 
 #include <algorithm>
@@ -53,7 +52,6 @@ constexpr int kGeTHMax = 1024;
 constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
-constexpr int kGeExtrap = 32;             // default cycles between extrapolation checks (ge.hip's host chunk)
 template <int NW>
 constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
 
@@ -79,7 +77,6 @@ struct GeRun {
   int pull;               // distribution solves by the lottery pull (AIY_OPT_HIST_PULL): deterministic
   double loose_hist;      // loose-bracketing histogram tolerance (AIY_OPT_GE_LOOSE_HIST)
   double* qb;             // [n_cal][S][n_a] pull form: the matvec input rows
-  double* vec4;           // [n_cal][4][S][n_a] S > 8: the pull form's Krylov vectors (r, p, v, t)
   int* ainv;              // [n_cal][S][n_a + 1] pull form: inverse lottery
   double* tab;            // [n_cal][kGeBufs][2][S][n_a + 1]
   double* mass;           // [n_cal][S][n_a]
@@ -297,7 +294,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
   double* Vw = lds_v + (size_t)wv * SMAX * kTile;   // this wave's V[s'][lane]
   const int ntile = (j1 - j0 + kTile - 1) / kTile;
   double dmax = 0.0;
-  if (SMAX <= 8 && src_m == nullptr) {   // terminal guess: IdentityFunction (AS:898) of mNextArray
+  if (src_m == nullptr) {   // terminal guess: IdentityFunction (AS:898) of mNextArray
 #pragma unroll 1
     for (int tile = wv; tile < ntile; tile += NW) {
       const int jr = j0 + tile * kTile + lane;
@@ -321,61 +318,6 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
       }
     }
     return 0.0;
-  }
-  if constexpr (SMAX > 8) {
-    // many states (configs[4]): each row's V is folded into the lane's S expectations as it
-    // is interpolated, E[s] += P[s, s'] V[s'] (register accumulation, in s' order; no LDS V
-    // tile: 25 rows x 64 nodes per wave would not fit beside the windows), then phase 2 per
-    // state with the previous tables' values loaded at the end
-    double E[SMAX];
-    auto begin = [&](int, int) __attribute__((always_inline)) {
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) E[s] = 0.0;
-    };
-    auto end = [&](int, int j, double a) __attribute__((always_inline)) {
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        if (s < S) {
-          double pm = 0.0, pc = 0.0;
-          if (track) {
-            pm = load_f64_agent(&src_m[(size_t)s * n1 + j + 1]);
-            pc = load_f64_agent(&src_c[(size_t)s * n1 + j + 1]);
-          }
-          const double c = inv_marg<PK>(beta * E[s], gam);   // AS:1485-1490
-          const double m = a + c;                              // AS:1499
-          store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], m);
-          store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
-          if (track) dmax = nan_max(dmax, nan_max(fabs(m - pm), fabs(c - pc)));
-          if (j == 0) {
-            store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
-            store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
-          }
-        }
-      }
-    };
-    auto fold = [&](int sp, double f) __attribute__((always_inline)) {
-      const double V = R * marg_u<PK>(f, gam);   // RnextArray * MargValueFuncCRRA
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s)
-        if (s < S) E[s] += uniform_f64(s_Pe[s * S + sp]) * V;
-    };
-    if (src_m == nullptr) {   // terminal guess: IdentityFunction (AS:898) of mNextArray
-      const int ntile = (j1 - j0 + kTile - 1) / kTile;
-#pragma unroll 1
-      for (int tile = wv; tile < ntile; tile += NW) {
-        const int jr = j0 + tile * kTile + lane;
-        const int j = jr < j1 ? jr : j1 - 1;
-        const double a = a_grid[j];
-        begin(tile, j);
-        for (int sp = 0; sp < S; ++sp) fold(sp, (R * a + s_Wl[sp]) * 1.0);
-        end(tile, j, a);
-      }
-      return 0.0;
-    }
-    ge_rows_pass<SMAX, NW>(S, n_a, j0, j1, a_grid, src_m, src_c, R, s_Wl, s_hint, lds_win,
-                           [&](int, int, int, int sp, double, double f) __attribute__((always_inline)) { fold(sp, f); },
-                           begin, end);
-    return dmax;
   }
   // tiles one after another per wave: the previous tables' values at the lane's node
   // (distance) in flight from the tile's start, V of the tile's rows (phase 1), then its
@@ -424,7 +366,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
 
 // The kernel's LDS at file scope, so the search loop, the EGM cycle and the lottery (their
 // own non-inlined functions, each with its own register allocation) address it directly.
-constexpr int kGeSmax = 25;   // the configs[4] shape (25-state Rouwenhorst) is the largest resident one
+constexpr int kGeSmax = 8;    // the largest resident state count (Table II: 7)
 extern __shared__ double ge_dyn[];                 // histogram: span buffer + v; EGM: V tiles + windows
 __shared__ double ge_s_part[kHkRed][kGeWavesMax];
 __shared__ double ge_s_res[kHkRed];
@@ -765,7 +707,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       // ---- lottery of the own columns on the final tables (hist.hip hist_lottery_kernel) ----
       tp = __builtin_amdgcn_s_memrealtime();
       ge_lottery_fn<SMAX, NW>(S, n_a, j0, j1, a_grid, tabm(st.buf[2]), tabc(st.buf[2]), R, st.steps > 0, LO, WL,
-                              SMAX > 8 || g.pull != 0);
+                              g.pull != 0);
       // ---- the distribution's start (own columns) ----
       if (st.fresh_mass) {
         const double u0 = 1.0 / ((double)S * n_a);
@@ -789,24 +731,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     }
     // ---- the stationary distribution: BiCGSTAB on (I - T) mass = 0 ----
     int mv;
-    if constexpr (SMAX > 8) {   // many states: the pull form with the Krylov vectors in HBM (hist_pull.h)
-      const size_t pts = (size_t)S * n_a;
-      double* vec = g.vec4 + (size_t)cal * 4 * pts;
-      HpArgs hp;
-      hp.G = G; hp.S = S; hp.n_a = n_a; hp.w = w; hp.j0 = j0; hp.j1 = j1;
-      hp.LO = to_global((const int*)LO); hp.WL = to_global((const double*)WL);
-      hp.lottery_fresh = true;
-      hp.A = to_global(g.ainv + (size_t)cal * S * (n_a + 1));
-      hp.X = to_global(X);
-      hp.R = to_global(vec); hp.P = to_global(vec + pts); hp.V = to_global(vec + 2 * pts); hp.T = to_global(vec + 3 * pts);
-      hp.ctr = to_global(ctr); hp.gran = to_global(gran); hp.Pc = to_global(g.P + (size_t)cal * S * S);
-      hp.tol = st.htol;
-      hp.max_iter = g.max_hist;
-      hp.err = to_global(g.err);
-      hp.stop_ctr = to_global((const unsigned*)(g.stop_at > 0 ? g.done_ctr : nullptr));
-      hp.stop_at = (unsigned)g.stop_at;
-      mv = hp_solve_lds<SMAX, TH>(hp, &nb, &ne);
-    } else {
+    {
       HkArgs hk;
       hk.G = G; hk.S = S; hk.n_a = n_a; hk.cap = g.cap; hk.w = w; hk.j0 = j0; hk.j1 = j1;
       hk.LO = to_global((const int*)LO); hk.WL = to_global((const double*)WL); hk.X = to_global(X);
@@ -923,41 +848,10 @@ static const void* ge_fn() {
 // Launch shape of the device-resident search for (n_cal, S, n_a): every calibration's
 // cluster resident at once (n_cal G workgroups, one per CU, within the handle's CU limit).
 static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
-  if (S < 1 || (S > 8 && S != kGeSmax) || n_a < 2 || n_cal < 1) return false;
+  if (S < 1 || S > kGeSmax || n_a < 2 || n_cal < 1) return false;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   if (h->cu_limit > 0) cus = std::min(cus, h->cu_limit);
-  if (S > 8) {   // configs[4]'s 25 states: the pull-form solve, every cluster as large as the device allows
-    // (opt-in: inlined into the search kernel the 25-state pull solve runs at ~270 us per matvec
-    // against ~100 us as its own kernel, so the host-driven loop is faster: 11.0 vs 8.3 GE solves/s)
-    if (!h->ge_resident_wide) return false;
-    p.th = 512;
-    p.kc = 1;
-    p.smax = kGeSmax;
-    p.sc = 0;
-    p.fn = ge_fn<kGeSmax, 0, 1, 512>();
-    hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, p.fn) != hipSuccess) return false;
-    int lds_dev = 0;
-    if (hipDeviceGetAttribute(&lds_dev, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess)
-      return false;
-    const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
-    if (fa.sharedSizeBytes + 4096 >= lds_total) return false;
-    p.lds = (lds_total - fa.sharedSizeBytes - 1024) / 256 * 256;
-    if (p.lds < (size_t)8 * 4 * kWin * sizeof(double)) return false;   // the EGM's row windows
-    const int max_own = std::min((int)(p.lds / (sizeof(int) * (size_t)S)) - 2, kGeMaxTiles * kTile);
-    if (max_own < 1) return false;
-    const int g_min = (n_a + max_own - 1) / max_own;
-    if (g_min > kHcMaxG || (long long)g_min * n_cal > cus) return false;
-    int G = std::max(g_min, std::min(kHcMaxG, cus / n_cal));
-    G = std::min(G, n_a);
-    p.nj = (n_a + G - 1) / G;
-    p.G = (n_a + p.nj - 1) / p.nj;
-    if (p.G > kHcMaxG || (long long)p.G * n_cal > cus || p.nj > max_own) return false;
-    p.cap = 0;
-    p.blocks = (p.G * n_cal + 7) / 8 * 8;
-    return true;
-  }
   const int g_min = (n_a + 2 * 512 - 1) / (2 * 512);
   // the cluster reductions (ge_reduce, hist_bicg.h) read at most kHcMaxG workgroups
   if (g_min > kHcMaxG || g_min > cus) return false;
@@ -994,7 +888,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 }
 
 struct GeScratch {
-  size_t tab, mass, pmass, pg, qb, ainv, vec4, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
+  size_t tab, mass, pmass, pg, qb, ainv, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
       evlog, bytes;
 };
 // Per-calibration arrays (kept across the rebalancing launches) first, then the per-launch
@@ -1008,7 +902,6 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_m
   L.tab = take((size_t)n_cal * kGeBufs * 2 * S * (n_a + 1) * sizeof(double));
   L.mass = take(pts * 8); L.pmass = take(pts * 8); L.pg = take(pts * 8); L.qb = take(pts * 8);
   L.ainv = take((size_t)n_cal * S * (n_a + 1) * sizeof(int));
-  L.vec4 = S > 8 ? take(4 * pts * 8) : take(0);
   L.lo = take(pts * 4); L.wlo = take(pts * 8);
   L.slab = take((size_t)cus * 2 * cap_max * sizeof(double));
   L.span = take((size_t)cus * 8 * 4 * sizeof(int));
@@ -1080,7 +973,6 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.pg = reinterpret_cast<double*>(base + L.pg);
   g.qb = reinterpret_cast<double*>(base + L.qb);
   g.ainv = reinterpret_cast<int*>(base + L.ainv);
-  g.vec4 = reinterpret_cast<double*>(base + L.vec4);
   g.pull = h->hist_pull;
   g.loose_hist = std::pow(10.0, -(double)h->ge_loose_hist);
   g.lo = reinterpret_cast<int*>(base + L.lo);

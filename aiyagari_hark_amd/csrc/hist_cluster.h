@@ -141,8 +141,6 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
 const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k, bool pull = false);
 // pull form (hist_pull.h) for S > 8: the kernel, and its dynamic LDS for n_own columns
 const void* hist_pull_pick(int S);
-// on-chip form (hist_onchip.h): one calibration per launch, every CU
-const void* hist_onchip_pick(int S);
 size_t hist_pull_lds(int S, int n_own);
 constexpr int kHpTH = 512;
 

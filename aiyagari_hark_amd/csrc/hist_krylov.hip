@@ -37,7 +37,6 @@
 #include "hist_cluster.h"
 #include "hist_bicg.h"
 #include "hist_pull.h"
-#include "hist_onchip.h"
 
 namespace aiy {
 
@@ -131,50 +130,6 @@ __global__ __launch_bounds__(TH) void hist_pull_kernel(HcRun r) {
   unsigned nb = 0, ne = 0;
   const int mv = hp_solve<SMAX, TH>(a, L, nb, ne);
   if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
-}
-
-// The on-chip form (hist_onchip.h): ONE calibration per launch on every CU, Krylov vectors in
-// registers, the matvec's planes in LDS.
-template <int SMAX, int TH>
-__global__ __launch_bounds__(TH) void hist_onchip_kernel(HcRun r) {
-  extern __shared__ __attribute__((aligned(16))) char ho_dyn[];
-  const int G = r.G, S = r.S, n_a = r.n_a;
-  const int w = blockIdx.x;   // one calibration per launch
-  const int cal = r.cal0;
-  const size_t row0 = (size_t)cal * S;
-  const size_t pts = (size_t)S * n_a;
-  double* vec = r.dbuf + (size_t)cal * 4 * pts;
-  HpArgs a;
-  a.G = G; a.S = S; a.n_a = n_a; a.w = w;
-  a.j0 = w * r.nj;
-  a.j1 = min(a.j0 + r.nj, n_a);
-  a.LO = to_global(r.lo + row0 * n_a);
-  a.WL = to_global(r.wlo + row0 * n_a);
-  a.lottery_fresh = false;
-  a.A = to_global(r.ainv + (size_t)cal * S * (n_a + 1));
-  a.X = to_global(r.mass + row0 * n_a);
-  a.R = to_global(vec);
-  a.P = to_global(vec + pts);
-  a.V = to_global((double*)nullptr);
-  a.T = to_global((double*)nullptr);
-  a.ctr = to_global(r.ctr);
-  a.gran = to_global(reinterpret_cast<unsigned long long*>(r.dist));
-  a.Pc = to_global(r.P + (size_t)cal * S * S);
-  a.tol = r.tolv ? r.tolv[cal] : r.tol;
-  a.max_iter = r.max_iter;
-  a.err = to_global(r.err);
-  a.stop_ctr = to_global((const unsigned*)nullptr);
-  a.stop_at = 0u;
-  unsigned nb = 0, ne = 0;
-  const int mv = ho_solve<SMAX, TH>(a, ho_dyn, nb, ne);
-  if (mv >= 0 && w == 0 && threadIdx.x == 0) r.iters_out[cal] = mv;
-}
-
-const void* hist_onchip_pick(int S) {
-  // the mix holds a column's S pull sums in registers: the 25-state shape has its own
-  if (S == 25) return reinterpret_cast<const void*>(hist_onchip_kernel<25, kHpTH>);
-  if (S <= 32) return reinterpret_cast<const void*>(hist_onchip_kernel<32, kHpTH>);
-  return nullptr;
 }
 
 const void* hist_pull_pick(int S) {

@@ -31,7 +31,6 @@
 #include "common.h"
 #include "internal.h"
 #include "hist_cluster.h"
-#include "hist_onchip.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -521,7 +520,6 @@ struct HcPlan {
   size_t lds = 0;
   const void* fn = nullptr;
   bool pull = false;   // hist_pull.h form (S > 8 BiCGSTAB)
-  bool onchip = false;   // hist_onchip.h form (S > 8 BiCGSTAB, one calibration per launch)
   bool pull_small = false;   // hk_solve's pull matvec (S <= 8, AIY_OPT_HIST_PULL)
 };
 
@@ -540,36 +538,6 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
   if (S > 32 || S < 1 || n_a < 2) return false;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
-  if (krylov && S > 8 && h->hist_onchip) {
-    // on-chip form (hist_onchip.h): one calibration per launch on every CU, its Krylov vectors in
-    // registers -- when a workgroup's points fit kHoPPT per thread and its planes fit LDS
-    const void* fn = hist_onchip_pick(S);
-    hipFuncAttributes fa;
-    int lds_dev = 0;
-    if (fn && hipFuncGetAttributes(&fa, fn) == hipSuccess &&
-        hipDeviceGetAttribute(&lds_dev, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) == hipSuccess) {
-      const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
-      const int G0 = std::min(std::min(cus, kHoMaxG), n_a);
-      const int nj = (n_a + G0 - 1) / G0;
-      const int G = (n_a + nj - 1) / nj;
-      const size_t lds = (ho_lds_bytes(S, nj) + 255) / 256 * 256;
-      if ((long long)S * nj <= (long long)kHoPPT * kHpTH && fa.sharedSizeBytes + lds + 1024 <= lds_total) {
-        p.pull = true;
-        p.onchip = true;
-        p.smax = 32;
-        p.th = kHpTH;
-        p.kc = 1;
-        p.cap = 0;
-        p.vblock = 0;
-        p.fn = fn;
-        p.G = G;
-        p.nj = nj;
-        p.cals_per_launch = 1;
-        p.lds = lds;
-        return true;
-      }
-    }
-  }
   if (krylov && S > 8) {   // pull form (hist_pull.h): vectors in HBM, every calibration at once
     p.pull = true;
     p.smax = 32;

@@ -42,13 +42,8 @@ struct aiy_handle {
   int hist_cluster_cap = 0;          // AIY_OPT_HIST_CLUSTER: max workgroups per calibration (0: 32)
   int hist_accel = 0;                // AIY_OPT_HIST_ACCEL: Aitken period of the resident histogram (0: off)
   int hist_krylov = 0;               // AIY_OPT_HIST_KRYLOV: resident histogram solves by BiCGSTAB
-  int res_fuse = 0;                  // AIY_OPT_RESIDENT_FUSE: streaming panel draws fused into the lookup pass
   int res_shape_stream = 1;          // AIY_OPT_RESIDENT_SHAPE_STREAM: shape of the HBM-streaming form (-1: res_shape)
-  int res_engine = 0;                // AIY_OPT_RESIDENT_ENGINE: streaming form by the loader ring (sim_stream_kernel)
-  int hist_onchip = 0;               // AIY_OPT_HIST_ONCHIP: S > 8 solves on chip, one calibration per launch
   int hist_pull = 0;                 // AIY_OPT_HIST_PULL: BiCGSTAB matvecs of S <= 8 by the lottery pull
-  bool ge_resident_wide = false;     // AIY_OPT_GE_RESIDENT_WIDE: the 25-state shape on the resident search too
-  bool ge_loose_brent = false;       // AIY_OPT_GE_LOOSE_BRENT: host-driven search, Brent's evaluations loose too
   int ge_loose_hist = 8;             // AIY_OPT_GE_LOOSE_HIST: loose-bracketing histogram tolerance 10^-value
   // per-calibration tolerances for one call (aiy_ge_stationary's loose bracketing); null: the
   // scalar tolerance of the call.  Device arrays [n_cal]; egm_tolh: the host copy.

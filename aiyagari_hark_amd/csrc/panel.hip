@@ -459,11 +459,6 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       return AIY_OK;
     case AIY_OPT_HIST_KRYLOV: h->hist_krylov = value != 0; return AIY_OK;
     case AIY_OPT_HIST_PULL: h->hist_pull = value != 0; return AIY_OK;
-    case AIY_OPT_RESIDENT_FUSE: h->res_fuse = value != 0; return AIY_OK;
-    case AIY_OPT_GE_RESIDENT_WIDE: h->ge_resident_wide = value != 0; return AIY_OK;
-    case AIY_OPT_RESIDENT_ENGINE: h->res_engine = value != 0; return AIY_OK;
-    case AIY_OPT_GE_LOOSE_BRENT: h->ge_loose_brent = value != 0; return AIY_OK;
-    case AIY_OPT_HIST_ONCHIP: h->hist_onchip = value != 0; return AIY_OK;
     case AIY_OPT_RESIDENT_SHAPE_STREAM:
       if (value < -1 || value > 2) return fail(h, AIY_ERR_ARG, "AIY_OPT_RESIDENT_SHAPE_STREAM must be -1, 0, 1 or 2");
       h->res_shape_stream = (int)value;
@@ -511,11 +506,6 @@ extern "C" int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value)
     case AIY_OPT_HIST_ACCEL: *value = h->hist_accel; return AIY_OK;
     case AIY_OPT_HIST_KRYLOV: *value = h->hist_krylov; return AIY_OK;
     case AIY_OPT_HIST_PULL: *value = h->hist_pull; return AIY_OK;
-    case AIY_OPT_RESIDENT_FUSE: *value = h->res_fuse; return AIY_OK;
-    case AIY_OPT_GE_RESIDENT_WIDE: *value = h->ge_resident_wide; return AIY_OK;
-    case AIY_OPT_RESIDENT_ENGINE: *value = h->res_engine; return AIY_OK;
-    case AIY_OPT_GE_LOOSE_BRENT: *value = h->ge_loose_brent; return AIY_OK;
-    case AIY_OPT_HIST_ONCHIP: *value = h->hist_onchip; return AIY_OK;
     case AIY_OPT_RESIDENT_SHAPE_STREAM: *value = h->res_shape_stream; return AIY_OK;
     case AIY_OPT_GE_LOOSE_HIST: *value = h->ge_loose_hist; return AIY_OK;
     case AIY_OPT_GE_RESIDENT: *value = h->ge_resident; return AIY_OK;

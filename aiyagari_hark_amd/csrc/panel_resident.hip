@@ -127,13 +127,7 @@ __host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
   return ((size_t)n_cells * sizeof(CellHdr) + 15) / 16 * 16;
 }
 
-// FUSE (HBM-streaming form): the next period's labour draws ride in the lookup pass -- the
-// agent's labour state is already in a register there, so one streaming pass per period
-// reads (a, l) and writes (a', l') instead of a second pass over the labour states.  The two
-// lanes of an agent pair (consecutive agents, one Philox call per pair) split the pairs of
-// their NA agents and swap halves with one DPP exchange, so each lane still runs one
-// Philox call per two agents.
-template <int TH, int NA, bool IN_LDS, bool QUAD, bool FUSE = false>
+template <int TH, int NA, bool IN_LDS, bool QUAD>
 __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
   extern __shared__ __attribute__((aligned(16))) char s_dyn[];
   __shared__ double s_cdf[kLdsLab * kLdsLab];
@@ -203,12 +197,12 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 
     // ---- 1. agents: lookups, a = m - c, partial sum ----
     double local = 0.0;
-    constexpr bool kPairs = !IN_LDS && !FUSE && NA % 2 == 0;
+    constexpr bool kPairs = !IN_LDS && NA % 2 == 0;
     for (int base = 0; base < cnt; base += TH * NA) {
       double m[NA];
       int ln[NA], cell[NA];
       // agent of slot k: consecutive lanes take consecutive agents (i = base + k TH + tid), except
-      // the unfused streaming form: agent PAIRS per lane (i = base + 2 (k/2 TH + tid) + k%2), so the
+      // the streaming form: agent PAIRS per lane (i = base + 2 (k/2 TH + tid) + k%2), so the
       // assets move as 16-byte loads / stores and the labour states as 2-byte ones
       if constexpr (kPairs) {
 #pragma unroll
@@ -298,46 +292,6 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
           local += an;
         }
       }
-      if constexpr (FUSE) {
-        if (p + 1 < r.n_periods) {   // period t + 1's labour from this period's (AS:1253-1254)
-          static_assert(NA % 2 == 0, "agent pairs split over the lane pair");
-          constexpr int H = NA / 2;
-          double u[NA];
-          const bool odd = (tid & 1) != 0;
-          if (r.u) {
-            const double* ut = r.u + (size_t)(t + 1 - r.t0) * r.u_ld + start;
-#pragma unroll
-            for (int k = 0; k < NA; ++k) {
-              const int i = base + k * TH + tid;
-              u[k] = i < cnt ? ut[i] : 0.0;
-            }
-          } else {
-            const unsigned ctr1 = (r.ge_iter << 20) | (unsigned)(t + 1);
-            double ue[H], uo[H];
-#pragma unroll
-            for (int h = 0; h < H; ++h) {   // even lane: pairs of its agents 0..H-1; odd lane: H..NA-1
-              const int k = odd ? h + H : h;
-              const long long i0 = r.offset + start + base + k * TH + (tid & ~1);
-#ifdef AIY_DIAG_NO_PHILOX
-              ue[h] = 0.37 + 1e-9 * (double)(i0 & 1023); uo[h] = 0.41 + 1e-9 * (double)(i0 & 1023);   // diagnostic
-#else
-              philox_uniform2(ctr1, (uint64_t)(i0 >> 1), r.seed, 0u, ue[h], uo[h]);
-#endif
-            }
-#pragma unroll
-            for (int h = 0; h < H; ++h) {
-              const double y = dpp_f64<kDppXor1>(odd ? ue[h] : uo[h]);   // the partner lane's half
-              u[h] = odd ? y : ue[h];
-              u[h + H] = odd ? uo[h] : y;
-            }
-          }
-#pragma unroll
-          for (int k = 0; k < NA; ++k) {
-            const int i = base + k * TH + tid;
-            if (i < cnt) L[i] = (uint8_t)draw_labour(s_cdf, n_lab, ln[k], u[k]);
-          }
-        }
-      }
     }
 
     // ---- 2. publish the workgroup partial as two tagged granules ----
@@ -361,7 +315,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #ifndef AIY_DRAW_MODE
 #define AIY_DRAW_MODE 2
 #endif
-    if (!FUSE && p + 1 < r.n_periods) {
+    if (p + 1 < r.n_periods) {
 #if AIY_DRAW_MODE == 0   // every wave draws, wave 0 then sweeps
       draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid, TH);
 #elif AIY_DRAW_MODE == 1   // wave 4 takes wave 0's pairs
@@ -453,335 +407,6 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
   }
 }
 
-// ---------------------------------------------------------------------------------
-// HBM-streaming form with a loader ring (slices far larger than LDS: configs[3]).
-//
-// In the plain streaming form every lane's pass is one dependent chain -- agent load
-// (HBM) -> bracket index -> record -> store -- and vmcnt retires in issue order, so the
-// HBM trip cannot leave that chain inside one wave.  Here the roles split by wave:
-//   waves 0..3 (one per SIMD) are LOADERS: per pass they stream the pass two ahead from
-//     HBM into an LDS ring slot (16-byte asset pieces, 4-byte labour words), and write the
-//     pass one behind back (a' and the next period's labour states from the slot);
-//   waves 4..15 are CONSUMERS: two agent pairs per lane from the slot -> m, the table
-//     lookup, a = m - c back into the slot, the partial sum (fixed order), and the next
-//     period's labour draws (Philox + inverse CDF, AS:1253-1254) into the slot.
-// Three slots: at pass g the consumers read slot g, the loaders write back g - 1 and refill
-// the same slot with g + 2 (each loader lane reads and rewrites only its own bytes).  The
-// agents of a workgroup split into passes of kStPass; passes run on through period ends
-// (the loaders prefetch the next period's first passes), which needs >= kStMinPasses passes
-// per period: the write-back of a pass must precede the prefetch of the same agents
-// (the same loader lane issues both, in program order).  Slices are balanced to multiples
-// of 16 agents (st_start).  Per period the exchange is the one of sim_resident_kernel.
-// ---------------------------------------------------------------------------------
-constexpr int kStTH = 1024;
-constexpr int kStLoadLanes = 4 * kWave;                // waves 0..3
-constexpr int kStCons = kStTH - kStLoadLanes;          // 768 consumer lanes
-constexpr int kStNA = 4;                               // agents per consumer lane per pass
-constexpr int kStPass = kStCons * kStNA;               // 3 072 agents per pass
-constexpr int kStSlots = 3;
-constexpr int kStA16 = kStPass / 2 / kStLoadLanes;     // 16-byte asset pieces per loader lane
-constexpr int kStLW = kStPass / 4 / kStLoadLanes;      // labour words per loader lane
-constexpr size_t kStSlotBytes = (size_t)kStPass * 9;
-constexpr int kStMinPasses = 4;
-static_assert(kStA16 * 2 * kStLoadLanes == kStPass && kStLW * 4 * kStLoadLanes == kStPass, "pass layout");
-static_assert(kStSlotBytes % 16 == 0, "slot alignment");
-
-// first agent of workgroup b of nb: balanced, a multiple of 16
-__host__ __device__ inline long long st_start(long long n, int nb, int b) {
-  return b >= nb ? n : ((long long)b * n / nb) & ~15LL;
-}
-
-template <bool QUAD>
-__global__ __launch_bounds__(kStTH) void sim_stream_kernel(PanelDev P, ResRun r, aiy_market mk) {
-  extern __shared__ __attribute__((aligned(16))) char s_dyn[];
-  __shared__ double s_cdf[kLdsLab * kLdsLab];
-  __shared__ double s_lvl[kLdsLab];
-  __shared__ double s_Mg[kResMaxM];
-  __shared__ double s_red[kStTH / kWave];
-  __shared__ double s_price[4];   // Mnow, Rnow, Wnow, Mrkv
-  __shared__ int s_abort;
-
-  const int tid = threadIdx.x;
-  const int nb = gridDim.x;
-  const int n_M = P.n_M, n_lab = P.n_lab, n_J = P.tab.g.n_J, n_cells = P.tab.g.n_cells;
-  const long long start = st_start(r.n, nb, blockIdx.x);
-  const int cnt = (int)(st_start(r.n, nb, blockIdx.x + 1) - start);
-  CellHdr* hdr = reinterpret_cast<CellHdr*>(s_dyn);
-  char* ring = s_dyn + res_hdr_bytes(n_cells);
-  double* A = r.a + start;
-  uint8_t* L = r.lab + start;
-
-  for (int q = tid; q < n_lab * n_lab; q += kStTH) s_cdf[q] = P.lab_cdf[q];
-  for (int q = tid; q < n_lab; q += kStTH) s_lvl[q] = P.lab_level[q];
-  for (int q = tid; q < n_M; q += kStTH) s_Mg[q] = P.M_grid[q];
-  for (int q = tid; q < n_cells; q += kStTH) hdr[q] = cell_header(P.tab, q);
-  if (tid == 0) {
-    s_price[0] = load_f64_agent(&r.sow[0]);
-    s_price[1] = load_f64_agent(&r.sow[3]);
-    s_price[2] = load_f64_agent(&r.sow[4]);
-    s_price[3] = load_f64_agent(&r.sow[2]);
-  }
-  __syncthreads();
-  draw_slice<kDrawGroup>(r, L, start, cnt, r.t0, s_cdf, n_lab, tid, kStTH);   // period t0's labour
-  __syncthreads();
-
-  const int Pn = (cnt + kStPass - 1) / kStPass;   // passes per period (>= kStMinPasses, host-checked)
-  const int Gtot = Pn * r.n_periods;
-  const bool loader = tid < kStLoadLanes;
-  const int lam = tid;                     // loader lane
-  const int cid = tid - kStLoadLanes;      // consumer lane
-  auto slot_a = [&](int g) { return reinterpret_cast<double*>(ring + (size_t)(g % kStSlots) * kStSlotBytes); };
-  auto slot_l = [&](int g) {
-    return reinterpret_cast<unsigned*>(ring + (size_t)(g % kStSlots) * kStSlotBytes + (size_t)kStPass * 8);
-  };
-
-  // ---- loader: pass g of the slice -> slot g (registers only inside one call) ----
-  auto fill = [&](int g) __attribute__((always_inline)) {
-    const int base = (g % Pn) * kStPass;
-    st_d2 va[kStA16];
-    unsigned vl[kStLW];
-#pragma unroll
-    for (int u = 0; u < kStA16; ++u) {
-      const int i = base + 2 * (lam + kStLoadLanes * u);
-      if (i + 1 < cnt) {
-        va[u] = __builtin_nontemporal_load(reinterpret_cast<const st_d2*>(A + i));
-      } else {
-        va[u].x = i < cnt ? A[i] : 0.0;   // tail: zeros stand in (not written back, not summed)
-        va[u].y = 0.0;
-      }
-    }
-    const int i0 = base + 4 * kStLW * lam;
-    if (i0 + 4 * kStLW <= cnt) {
-#pragma unroll
-      for (int k = 0; k < kStLW; ++k) vl[k] = __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(L + i0) + k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kStLW; ++k) {
-        unsigned w = 0;
-        for (int b = 0; b < 4; ++b)
-          if (i0 + 4 * k + b < cnt) w |= (unsigned)L[i0 + 4 * k + b] << (8 * b);
-        vl[k] = w;
-      }
-    }
-    return [=, &slot_a, &slot_l]() __attribute__((always_inline)) {   // the LDS half, issued later
-      double* sa = slot_a(g);
-      unsigned* sl = slot_l(g);
-#pragma unroll
-      for (int u = 0; u < kStA16; ++u) *reinterpret_cast<st_d2*>(sa + 2 * (lam + kStLoadLanes * u)) = va[u];
-#pragma unroll
-      for (int k = 0; k < kStLW; ++k) sl[kStLW * lam + k] = vl[k];
-    };
-  };
-  // ---- loader: slot g -> HBM (a'; labour of the next period drawn on the way) ----
-  auto drain = [&](int g) __attribute__((always_inline)) {
-    const int base = (g % Pn) * kStPass;
-    const int p = g / Pn;
-    const double* sa = slot_a(g);
-#pragma unroll
-    for (int u = 0; u < kStA16; ++u) {
-      const int i = base + 2 * (lam + kStLoadLanes * u);
-      const st_d2 v = *reinterpret_cast<const st_d2*>(sa + 2 * (lam + kStLoadLanes * u));
-      if (i + 1 < cnt) __builtin_nontemporal_store(v, reinterpret_cast<st_d2*>(A + i));
-      else if (i < cnt) A[i] = v.x;
-    }
-    if (p + 1 < r.n_periods) {   // period t + 1's labour states (drawn by the consumers)
-      const unsigned* sl = slot_l(g);
-      const int i0 = base + 4 * kStLW * lam;
-      if (i0 + 4 * kStLW <= cnt) {
-#pragma unroll
-        for (int k = 0; k < kStLW; ++k)
-          __builtin_nontemporal_store(sl[kStLW * lam + k], reinterpret_cast<unsigned*>(L + i0) + k);
-      } else {
-        const uint8_t* sb = reinterpret_cast<const uint8_t*>(sl) + 4 * kStLW * lam;
-        for (int b = 0; b < 4 * kStLW; ++b)
-          if (i0 + b < cnt) L[i0 + b] = sb[b];
-      }
-    }
-  };
-
-  // ---- consumers: the period's prices ----
-  double Rnow = 0.0, Wnow = 0.0, alpha = 0.0;
-  int Mrkv = 0, jc = 0;
-  auto period_prices = [&]() {
-    Rnow = s_price[1];
-    Wnow = s_price[2];
-    Mrkv = (int)s_price[3];
-    m_bracket(s_Mg, n_M, s_price[0], jc, alpha);
-  };
-
-  if (loader) {
-    auto put0 = fill(0);
-    put0();
-    if (Gtot > 1) {
-      auto put1 = fill(1);
-      put1();
-    }
-  }
-  period_prices();
-  __syncthreads();
-
-  double local = 0.0;
-  Prices last{};
-#ifdef AIY_DIAG_PHASES
-  unsigned long long d_work = 0, d_bar = 0, d_per = 0, d_t = 0;   // diagnostic build: 100 MHz ticks
-#define AIY_ST(v) do { const unsigned long long tn = __builtin_amdgcn_s_memrealtime(); v += tn - d_t; d_t = tn; } while (0)
-  d_t = __builtin_amdgcn_s_memrealtime();
-#else
-#define AIY_ST(v) do {} while (0)
-#endif
-  for (int g = 0; g < Gtot; ++g) {
-    if (loader) {
-      if (g + 2 < Gtot) {
-        auto put = fill(g + 2);       // HBM loads in flight across the write-back
-        if (g >= 1) drain(g - 1);
-        put();
-      } else if (g >= 1) {
-        drain(g - 1);
-      }
-    } else {
-      // consumer lane: agent pairs (2 cid + 2 kStCons kp) + {0, 1} of the slot
-      const int base = (g % Pn) * kStPass;
-      const int p = g / Pn;
-      double* sa = slot_a(g);
-      uint8_t* sl = reinterpret_cast<uint8_t*>(slot_l(g));
-      double m[kStNA], c[kStNA];
-      int cell[kStNA], ln[kStNA];
-#pragma unroll
-      for (int kp = 0; kp < kStNA / 2; ++kp) {
-        const int pos = 2 * (cid + kStCons * kp);
-        const st_d2 av = *reinterpret_cast<const st_d2*>(sa + pos);
-        const unsigned lv = *reinterpret_cast<const unsigned short*>(sl + pos);
-        ln[2 * kp] = (int)(lv & 0xffu);
-        ln[2 * kp + 1] = (int)(lv >> 8);
-        m[2 * kp] = Rnow * av.x + Wnow * (s_lvl[ln[2 * kp]] * 1.0);                        // AS:1283
-        m[2 * kp + 1] = Rnow * av.y + Wnow * (s_lvl[ln[2 * kp + 1]] * 1.0);
-      }
-#pragma unroll
-      for (int k = 0; k < kStNA; ++k) cell[k] = (2 * ln[k] + Mrkv) * n_J + jc;             // employed (Urate = 0)
-      tab_policy<kStNA, QUAD>(P.tab, cell, hdr, cell, m, alpha, n_M > 1, c);                // AS:1326-1408
-#pragma unroll
-      for (int kp = 0; kp < kStNA / 2; ++kp) {
-        const int pos = 2 * (cid + kStCons * kp);
-        st_d2 an;
-        an.x = m[2 * kp] - c[2 * kp];                                                      // AS:1415
-        an.y = m[2 * kp + 1] - c[2 * kp + 1];
-        *reinterpret_cast<st_d2*>(sa + pos) = an;
-        if (base + pos < cnt) local += an.x;
-        if (base + pos + 1 < cnt) local += an.y;
-      }
-      if (p + 1 < r.n_periods) {   // period t + 1's labour states from period t's (AS:1253-1254)
-        const int t1 = r.t0 + p + 1;
-        const unsigned ctr1 = (r.ge_iter << 20) | (unsigned)t1;
-        const double* ut = r.u ? r.u + (size_t)(t1 - r.t0) * r.u_ld + start : nullptr;
-#pragma unroll
-        for (int kp = 0; kp < kStNA / 2; ++kp) {
-          const int pos = 2 * (cid + kStCons * kp);
-          const int i = base + pos;
-          double u0, u1;
-          if (ut) {
-            u0 = i < cnt ? ut[i] : 0.0;
-            u1 = i + 1 < cnt ? ut[i + 1] : 0.0;
-          } else {
-            philox_uniform2(ctr1, (uint64_t)((r.offset + start + i) >> 1), r.seed, 0u, u0, u1);
-          }
-          const int n0 = draw_labour(s_cdf, n_lab, ln[2 * kp], u0);
-          const int n1 = draw_labour(s_cdf, n_lab, ln[2 * kp + 1], u1);
-          *reinterpret_cast<unsigned short*>(sl + pos) = (unsigned short)(n0 | (n1 << 8));
-        }
-      }
-    }
-    AIY_ST(d_work);
-    __syncthreads();
-    AIY_ST(d_bar);
-    if (g % Pn != Pn - 1) continue;
-
-    // ---- end of period p: partial sums, exchange, prices (as sim_resident_kernel) ----
-    const int p = g / Pn;
-    const int t = r.t0 + p;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
-    if ((tid & (kWave - 1)) == 0) s_red[tid / kWave] = local;
-    local = 0.0;
-    __syncthreads();
-    const unsigned e = (unsigned)p + 1;
-    unsigned long long* gslot = r.gran + (size_t)(p & 1) * 2 * nb;
-    if (tid == kStLoadLanes) {
-      double sb = 0.0;
-      for (int w = 0; w < kStTH / kWave; ++w) sb += s_red[w];
-      const unsigned long long bits = (unsigned long long)__double_as_longlong(sb);
-      __hip_atomic_store(to_global(&gslot[2 * blockIdx.x]), ((unsigned long long)e << 32) | (bits >> 32), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(to_global(&gslot[2 * blockIdx.x + 1]), ((unsigned long long)e << 32) | (bits & 0xffffffffull),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid >= kStLoadLanes && tid < kStLoadLanes + kWave) {   // wave 4 sweeps
-      const int sl = tid - kStLoadLanes;
-      const int mrkv_next = P.mrkv_hist[t];
-      unsigned long long gv[kResGranPerLane];
-      const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-      int ok = 1;
-      for (;;) {
-        bool all = true;
-#pragma unroll
-        for (int k = 0; k < kResGranPerLane; ++k) {
-          const int gi = sl * kResGranPerLane + k;
-          if (gi < 2 * nb) {
-            gv[k] = __hip_atomic_load(to_global(&gslot[gi]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            all = all && (unsigned)(gv[k] >> 32) == e;
-          } else {
-            gv[k] = 0;
-          }
-        }
-        if (__all(all)) break;
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t_start > kResTimeoutTicks) { ok = 0; break; }
-      }
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < kResGranPerLane; k += 2) {
-        const unsigned long long bits = ((gv[k] & 0xffffffffull) << 32) | (gv[k + 1] & 0xffffffffull);
-        acc += __longlong_as_double((long long)bits);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
-      if (sl == 0) {
-        if (!ok) __hip_atomic_store(to_global(r.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_abort = ok ? 0 : 1;
-        last = calc_prices(mk, mrkv_next, acc / (double)r.n);   // np.mean(np.array(aNow))
-        s_price[0] = last.Mnow;
-        s_price[1] = last.Rnow;
-        s_price[2] = last.Wnow;
-        s_price[3] = (double)last.Mrkv;
-        if (blockIdx.x == 0) {
-          if (r.hist_A) r.hist_A[t] = last.Aprev;
-          if (r.hist_M) r.hist_M[t] = last.Mnow;
-        }
-      }
-    }
-    __syncthreads();
-    if (s_abort) return;   // sweep timeout: the host reports it (tmo word)
-    period_prices();
-    AIY_ST(d_per);
-  }
-  if (loader && Gtot > 0) drain(Gtot - 1);
-#ifdef AIY_DIAG_PHASES
-  if ((tid == 0 || tid == kStLoadLanes) && (blockIdx.x == 0 || blockIdx.x == nb - 1))
-    printf("[ring] block %d %s: work %.2f barrier %.2f period-end %.2f us/period (%d passes/period)\n", blockIdx.x,
-           tid == 0 ? "loader" : "consumer", d_work * 0.01 / r.n_periods, d_bar * 0.01 / r.n_periods,
-           d_per * 0.01 / r.n_periods, Pn);
-#endif
-#undef AIY_ST
-  if (blockIdx.x == 0 && tid == kStLoadLanes && r.n_periods > 0) {
-    r.sow[0] = last.Mnow;
-    r.sow[1] = last.Aprev;
-    r.sow[2] = (double)last.Mrkv;
-    r.sow[3] = last.Rnow;
-    r.sow[4] = last.Wnow;
-    r.sow[5] = 0.0;
-    r.sow[7] = (double)(r.t0 + r.n_periods);
-  }
-}
-
 // Workgroup shape (threads per workgroup, agents per lane per pass, record loads) by
 // handle option: 0 -> 512 x 8 quad-cooperative (default: a ~4k-agent slice in ONE pass,
 // 256 VGPRs), 1 -> 1024 x 4 quad-cooperative, 2 -> 512 x 8 per-lane record loads.
@@ -858,40 +483,6 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   }
   int32_t rc = ensure_res_scratch(h);
   if (rc) return rc;
-  // the loader-ring streaming form (sim_stream_kernel): balanced 16-agent-aligned slices of
-  // >= kStMinPasses passes, 16-byte aligned assets and labour states
-  const long long st_min = (long long)kStMinPasses * kStPass + 16;   // agents per slice
-  const int nb_st = (int)std::max(1LL, std::min<long long>(G.nb, n / st_min));
-  const bool ring = !G.in_lds && h->res_engine && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(lab)) & 15) == 0 &&
-                    n >= st_min;
-  if (ring) {
-    const void* fn = reinterpret_cast<const void*>(sim_stream_kernel<true>);
-    const size_t lds = res_hdr_bytes(P.tab.g.n_cells) + kStSlots * kStSlotBytes;
-    static bool st_attr = false;
-    if (!st_attr) {
-      AIY_HIP(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
-      st_attr = true;
-    }
-    if (lds > kResLdsBudget) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: ring does not fit LDS");
-    ResRun r;
-    r.n = n; r.offset = 0; r.chunk = 0; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld; r.seed = seed;
-    r.ge_iter = ge_iter; r.t0 = t0; r.n_periods = n_periods; r.sow = sow;
-    r.gran = reinterpret_cast<unsigned long long*>(h->d_res_sync);
-    r.tmo = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes);
-    r.hist_A = hist_A; r.hist_M = hist_M;
-    PanelDev Pc = P;
-    aiy_market mkc = mk;
-    AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
-    void* args[] = {&Pc, &r, &mkc};
-    int per_cu = 0;
-    AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kStTH, lds));
-    if (per_cu < 1) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: ring workgroup does not fit a CU");
-    AIY_HIP(h, hipEventRecord(h->res_ev[0], st));
-    AIY_HIP(h, hipLaunchKernel(fn, dim3(nb_st), dim3(kStTH), args, lds, st));
-    AIY_HIP(h, hipEventRecord(h->res_ev[1], st));
-    h->res_periods += n_periods;
-    return AIY_OK;
-  }
   const void* kernels[3][2] = {
       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true>),
        reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, true>)},
@@ -899,17 +490,11 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
        reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true>)},
       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false>),
        reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false>)}};
-  // streaming form with the labour draws fused into the lookup pass (AIY_OPT_RESIDENT_FUSE)
-  const void* fused[3] = {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true, true>),
-                          reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false, true, true>),
-                          reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false, true>)};
   static bool attr_set = false;
   if (!attr_set) {
     for (auto& row : kernels)
       for (const void* k : row)
         AIY_HIP(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
-    for (const void* k : fused)
-      AIY_HIP(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLdsBudget));
     attr_set = true;
   }
   ResRun r;
@@ -922,7 +507,7 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   aiy_market mkc = mk;
   AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
-  const void* fn = G.in_lds ? kernels[sh.id][1] : (h->res_fuse ? fused[sh.id] : kernels[sh.id][0]);
+  const void* fn = kernels[sh.id][G.in_lds ? 1 : 0];
   // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
   // against the occupancy query; a plain launch then has the same residency as a
   // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),

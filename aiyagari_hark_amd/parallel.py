@@ -73,13 +73,25 @@ def bind_rccl(handle: "_lib.Handle", group=None, prefer_torch=True):
     torch's collectives are ordered on one comm; else (or when torch's is not available)
     create the library's own (rank 0 makes the ncclUniqueId, torch.distributed broadcasts it).
     Returns (world, rank, "torch" | "own")."""
+    import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if prefer_torch:
+        nccl = dist.get_backend(group) == "nccl"
+        dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+        flag = torch.ones(1, dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, group=group)   # creates a lazily made communicator on every rank
         ptr = torch_comm_ptr(group)
-        if ptr is not None and handle.lib.aiy_comm_bind(handle.h, ctypes.c_void_p(ptr)) == _lib.AIY_OK:
+        ok = ptr is not None and handle.lib.aiy_comm_bind(handle.h, ctypes.c_void_p(ptr)) == _lib.AIY_OK
+        # every rank takes the same path: if any rank could not bind torch's communicator, the
+        # ranks that did unbind it and all of them create the library's own below
+        flag.fill_(1 if ok else 0)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if int(flag.item()) == 1:
             return world, rank, "torch"
+        if ok:
+            handle.check(handle.lib.aiy_comm_destroy(handle.h), "aiy_comm_destroy")
     buf = ctypes.create_string_buffer(128)
     if rank == 0:
         rc = handle.lib.aiy_comm_unique_id(buf)

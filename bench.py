@@ -507,13 +507,8 @@ def configs4_leg(args, world, rank, dev):
 
     share = cu_share(world)
 
-    resident = None if args.c4_resident < 0 else bool(args.c4_resident)
-    if resident:   # the 25-state shape on the resident search is opt-in (AIY_OPT_GE_RESIDENT_WIDE)
-        h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
-
     def solve():
-        return (solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share, resident=resident)
-                if cals else None)
+        return solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share) if cals else None
 
     solve()   # warm-up
     hist_stats(h, True, dev)
@@ -524,18 +519,11 @@ def configs4_leg(args, world, rank, dev):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     hist_ms, hist_n = hist_stats(h, True, dev)
-    ge_ms, ge_n, ge_pts, ge_cyc = ge_stats(h, True, dev)
-    if ge_n > 0:   # the device-resident search (ge_cluster_kernel<25, ...>, pull-form solves)
-        kern = ("ge_cluster_kernel<25, 0, 1, 512> (device-resident GE search: EGM cycles + lottery + pull-form "
-                "BiCGSTAB + root search)")
-        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * ge_pts + EGM_BYTES_PER_NODE_CYCLE * 25 * (n_a + 1) * ge_cyc
-        hist_ms, hist_n = ge_ms, ge_n
-        trace_name = "ge_cluster_kernel"
-    else:          # host-driven loop: the pull-form distribution solve is the dominant kernel
-        kern = "hist_pull_kernel<32, 512> (pull-form BiCGSTAB distribution solve, Krylov vectors in HBM)"
-        pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
-        hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
-        trace_name = "hist_pull_kernel"
+    # the host-driven loop (S > 8): the pull-form distribution solve is the dominant kernel
+    kern = "hist_pull_kernel<32, 512> (pull-form BiCGSTAB distribution solve, Krylov vectors in HBM)"
+    pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
+    hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
+    trace_name = "hist_pull_kernel"
     gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[] if res is None else [float(x) for x in res.r],
                                    status=[] if res is None else [int(x) for x in res.status]), world)
@@ -742,12 +730,8 @@ def main():
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     ap.add_argument("--ge-rebalance", type=int, default=None,
                     help="AIY_OPT_GE_REBALANCE for the resident searches (default: the library's)")
-    ap.add_argument("--c4-resident", type=int, default=-1,
-                    help="configs4: 1 the device-resident search, 0 the host-driven loop, -1 the default")
     ap.add_argument("--ge-loose-hist", type=int, default=None,
                     help="AIY_OPT_GE_LOOSE_HIST (loose-bracketing histogram tolerance 10^-v; default the library's)")
-    ap.add_argument("--ge-loose-brent", type=int, default=None,
-                    help="AIY_OPT_GE_LOOSE_BRENT (host-driven search: Brent's evaluations loose too)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
@@ -762,8 +746,7 @@ def main():
         build.build(verbose=False)
     barrier(world)
     legs = set(args.legs.split(","))
-    if (args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None or
-            args.ge_loose_brent is not None):
+    if args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None:
         from aiyagari_hark_amd import _lib
         opts = {}
         if args.hist_pull is not None:
@@ -772,8 +755,6 @@ def main():
             opts[_lib.AIY_OPT_GE_REBALANCE] = args.ge_rebalance
         if args.ge_loose_hist is not None:
             opts[_lib.AIY_OPT_GE_LOOSE_HIST] = args.ge_loose_hist
-        if args.ge_loose_brent is not None:
-            opts[_lib.AIY_OPT_GE_LOOSE_BRENT] = args.ge_loose_brent
         _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]

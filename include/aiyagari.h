@@ -368,33 +368,15 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     PULLING each destination's lottery sources in ascending order
                                     (hist_pull.h's inverse lottery) instead of LDS-atomic pushes:
                                     deterministic run to run; 0: the push form.  S > 8 always pulls */
-#define AIY_OPT_RESIDENT_FUSE 16   /* value != 0: the HBM-streaming form of the resident panel draws the
-                                    next period's labour states inside the lookup pass (one pass over
-                                    the agents per period); 0 (default): a separate draw pass (faster
-                                    with the default streaming shape) */
 #define AIY_OPT_GE_LOOSE_HIST 17   /* value v in [6, 14] (default 8): the loose-bracketing evaluations'
                                     distribution tolerance is 10^-v (their sign needs |K_s - K_d| >= 5 %
                                     of K_d; the final bracket's evaluations use the full tolerance) */
 #define AIY_OPT_RESIDENT_SHAPE_STREAM 18 /* workgroup shape (AIY_OPT_RESIDENT_SHAPE's values) of the resident
                                     panel's HBM-streaming form (agents beyond LDS, e.g. configs[3]);
                                     default 1 (1024 threads x 4 agents); -1: AIY_OPT_RESIDENT_SHAPE */
-#define AIY_OPT_GE_RESIDENT_WIDE 19 /* value != 0: the device-resident search also takes the 25-state shape
-                                    (configs[4]; pull-form solves inlined into the search kernel); 0
-                                    (default): that shape runs the host-driven loop, which is faster */
-#define AIY_OPT_RESIDENT_ENGINE 20 /* value != 0: the resident panel's HBM-streaming form runs as a loader
-                                    ring (4 loader waves stream the agents through LDS, 12 consumer
-                                    waves look up; slower at configs[3]: 1 420 vs 1 002 us per period);
-                                    0 (default): every wave streams its own agents
-                                    (AIY_OPT_RESIDENT_SHAPE_STREAM) */
-#define AIY_OPT_GE_LOOSE_BRENT 21  /* value != 0: the host-driven search (aiy_ge_stationary without the
-                                    device-resident search) also runs Brent's evaluations at the loose
-                                    tolerances, refining any whose |K_s - K_d| is below the sign
-                                    margin; 0 (default): loose during bracketing only */
-#define AIY_OPT_HIST_ONCHIP 22     /* value != 0: distribution solves with S > 8 states run one calibration
-                                    per launch on every CU with the BiCGSTAB vectors on chip (registers
-                                    + LDS) when a workgroup's share fits (slower at configs[4]: its
-                                    256-workgroup barriers and reductions); 0 (default): all
-                                    calibrations at once, vectors in HBM (the pull form) */
+/* (options 16, 19, 20, 21 and 22 -- fused panel draws, the 25-state resident search, the
+   loader-ring panel, loose Brent evaluations, the on-chip S > 8 solve -- were measured slower
+   than the defaults and removed in round 5; setting them returns AIY_ERR_ARG) */
 int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value);
 /* The current value of an option (so a caller can save and restore what it changes). */
 int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value);
@@ -466,7 +448,8 @@ typedef struct {
                             unchanged; iterates differ from the Python-driven loop)          */
   int32_t loose_bracket; /* != 0 (method 1): while a calibration's search is still bracketing
                             (bisection before the first sign change) its evaluations run to
-                            the looser tolerances egm 1e-6 / hist 1e-10; the sign of
+                            the looser tolerances egm 1e-6 / hist 10^-AIY_OPT_GE_LOOSE_HIST
+                            (default 1e-8); the sign of
                             K_s - K_d is taken only where |K_s - K_d| >= 5 % of K_d, else
                             the same r is evaluated again at the full tolerances          */
   int32_t egm_extrapolate; /* != 0: the household solves move a calibration's tables along

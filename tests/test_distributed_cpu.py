@@ -113,3 +113,78 @@ def test_sharded_panel_equals_single_shard():
     assert np.allclose(res[1][0], hist1, rtol=1e-13, atol=0)
     assert np.array_equal(np.concatenate([res[0][2], res[1][2]]), l1)
     assert np.allclose(np.concatenate([res[0][1], res[1][1]]), a1, rtol=1e-12)
+
+
+class _FakeLib:
+    """Stand-in for libaiyagari's communicator entry points (host logic only)."""
+
+    def __init__(self, bind_ok):
+        self.bind_ok = bind_ok
+        self.calls = []
+
+    def aiy_comm_bind(self, h, ptr):
+        self.calls.append("bind")
+        return 0 if self.bind_ok else -5
+
+    def aiy_comm_destroy(self, h):
+        self.calls.append("destroy")
+        return 0
+
+    def aiy_comm_unique_id(self, buf):
+        self.calls.append("uid")
+        buf.raw = bytes(range(128))
+        return 0
+
+    def aiy_comm_init(self, h, uid, world, rank):
+        self.calls.append(("init", bytes(uid.raw[:4]), world, rank))
+        return 0
+
+
+class _FakeHandle:
+    def __init__(self, lib):
+        self.lib = lib
+        self.h = None
+
+    def check(self, rc, what):
+        assert rc == 0, what
+
+
+def _bind_worker(rank, world, port, out_q, ok_ranks):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        par.torch_comm_ptr = lambda group=None, device=None: 0x1234   # a communicator to lend
+        lib = _FakeLib(rank in ok_ranks)
+        out = par.bind_rccl(_FakeHandle(lib))
+        out_q.put((rank, out, lib.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("ok_ranks", [(0, 1), (0,)])
+def test_bind_rccl_ranks_agree(ok_ranks):
+    """bind_rccl: when one rank cannot bind torch's communicator, every rank takes the
+    library's own (the ranks that bound unbind first), so no rank waits in a broadcast the
+    others never join."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_bind_worker, args=(r, world, port, q, ok_ranks)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, c)) for r, o, c in (q.get(timeout=100) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kinds = {res[r][0][2] for r in range(world)}
+    assert len(kinds) == 1
+    if len(ok_ranks) == world:
+        assert kinds == {"torch"}
+    else:
+        assert kinds == {"own"}
+        assert "destroy" in res[0][1] and "destroy" not in res[1][1]
+        for r in range(world):
+            assert ("init", bytes(range(4)), world, r) in res[r][1]

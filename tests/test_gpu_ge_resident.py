@@ -36,14 +36,8 @@ def test_resident_plan_shapes(gpu):
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
     from aiyagari_hark_amd import _lib
     h = _lib.handle(gpu.index)
-    assert resident_plan(gpu, 3, 25, 50_000) is None     # configs[4] by default: the host loop (faster)
-    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
-    try:
-        p25 = resident_plan(gpu, 3, 25, 50_000)          # opt-in: every stress cell resident at once
-        assert p25 is not None and p25[0] * 3 <= cus and p25[2] == 1
-        assert resident_plan(gpu, 3, 16, 50_000) is None  # other S > 8: the host loop
-    finally:
-        h.set_options(prev)
+    assert resident_plan(gpu, 3, 25, 50_000) is None     # configs[4]: the host-driven loop
+    assert resident_plan(gpu, 3, 16, 50_000) is None     # every S > 8: the host-driven loop
     # clusters above 128 workgroups would escape the cluster reductions: the host loop runs
     assert resident_plan(gpu, 1, 7, 150_000) is None
     p1 = resident_plan(gpu, 1, 7, 120_000)
@@ -170,24 +164,3 @@ def test_pull_matvec_sweep_deterministic(gpu, n_a):
     assert np.all(a.status == 0) and np.all(b.status == 0)
     assert np.array_equal(a.r, b.r) and np.array_equal(a.K_supply, b.K_supply)
     assert np.max(np.abs(a.r - push.r)) <= 2e-7
-
-
-def test_resident_stress_matches_host_search(gpu):
-    """The 25-state resident search (register-accumulated EGM expectations, pull-form
-    distribution solves) against the host-driven loop on the stress cells at N_a = 6 000:
-    the same roots within the search tolerance."""
-    from aiyagari_hark_amd.stationary import Calibration, solve_table2
-    cals = [Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=c, LaborStatesNo=25, income="rouwenhorst") for c in (1.0, 3.0, 5.0)]
-    from aiyagari_hark_amd import _lib
-    h = _lib.handle(gpu.index)
-    kw = dict(n_a=6000, device=gpu, method="brent")
-    prev = h.set_options({_lib.AIY_OPT_GE_RESIDENT_WIDE: 1})
-    try:
-        res = solve_table2(cals, resident=True, **kw)
-    finally:
-        h.set_options(prev)
-    ref = solve_table2(cals, resident=False, groups=1, **kw)
-    print(f"\nstress resident r {100 * res.r} host r {100 * ref.r}; evaluations {res.bisection_steps}")
-    assert np.all(res.status == 0) and np.all(ref.status == 0)
-    assert np.max(np.abs(res.r - ref.r)) <= 2e-7
-    assert np.max(np.abs(res.KtoY - ref.KtoY) / ref.KtoY) <= 2e-6

@@ -51,7 +51,6 @@ for step in "$@"; do
     pull7) run pull7 400 $PYT -s tests/test_gpu_hist_resident.py tests/test_gpu_ge_resident.py -k "pull" ;;
     t2pull) run t2pull 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --hist-pull 1 ;;
     t2push) run t2push 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --hist-pull 0 ;;
-    res25) run res25 400 $PYT -s tests/test_gpu_ge_resident.py -k "stress or plan_shapes" ;;
     panelfuse3) run panelfuse3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,1,0,200],[1,0,2,0,200]]' FUSE=1 python -u tools/panel_variants.py ;;
     panelnofuse3) run panelnofuse3 400 env NAG=99999998 T=200 OPTS='[[1,0,0,0,200],[1,0,1,0,200],[1,0,2,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     t2q34) run t2q34 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 34 ;;
@@ -59,19 +58,14 @@ for step in "$@"; do
     t2q25) run t2q25 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 25 ;;
     t2lh8) run t2lh8 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 8 ;;
     t2lh9) run t2lh9 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 9 ;;
-    c4host) run c4host 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --c4-resident 0 ;;
-    c4res) run c4res 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --c4-resident 1 ;;
     profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
     t2lh7) run t2lh7 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 7 ;;
     lgnt) for e in 1 0; do run lgnt$e 500 env ENGINE=$e NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=lg11=aiyagari_hark_amd/lib/variants/libaiyagari_lg11.so,lg12=aiyagari_hark_amd/lib/variants/libaiyagari_lg12.so,nt=aiyagari_hark_amd/lib/variants/libaiyagari_nt.so python -u tools/panel_variants.py; done ;;
     sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
-    c4lb) run c4lb0 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline && run c4lb1 300 python -u bench.py --legs configs4 --steps 3 --warmup 1 --no-cpu-baseline --ge-loose-brent 1 ;;
     sub8) run sub8_32 400 python -u tools/table2_rank_subsets.py 8 32 && run sub8_85 400 python -u tools/table2_rank_subsets.py 8 85 ;;
     sub8b) run sub8_16 400 python -u tools/table2_rank_subsets.py 8 16 && run sub8_24 400 python -u tools/table2_rank_subsets.py 8 24 && run sub8_48 400 python -u tools/table2_rank_subsets.py 8 48 ;;
     g3) run g3 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0 ;;
-    onchip) run onchip 500 $PYT tests/test_gpu_benchsize.py::test_stress_ge_matches_oracle_fullsize tests/test_gpu_benchsize.py::test_stress_capital_supply_at_oracle_root tests/test_gpu_parity.py::test_rouwenhorst_25_state_histogram ;;
-    occheck) run occheck 300 python -u tools/onchip_check.py 50000 ;;
     ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     panel3) run panel3 300 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 python -u tools/panel_variants.py ;;
     panelvar3s1) run panelvar3s1 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=nophilox=aiyagari_hark_amd/lib/variants/libaiyagari_nophilox.so,nolookup=aiyagari_hark_amd/lib/variants/libaiyagari_nolookup.so,phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
