@@ -36,6 +36,20 @@ def sources():
     return [f for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
 
 
+def source_digest() -> str:
+    """sha256 (first 16 hex digits) of every source the library is built from (csrc/*, the
+    ABI header): profiles/pmc_traffic.json stamps each PMC pass with it, and bench.py
+    reports a pass's traffic only while the sources are still the ones profiled."""
+    import hashlib
+    hsh = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    for f in files:
+        hsh.update(f.encode())
+        hsh.update(open(os.path.join(CSRC, f), "rb").read())
+    hsh.update(open(os.path.join(HERE, "..", "include", "aiyagari.h"), "rb").read())
+    return hsh.hexdigest()[:16]
+
+
 def needs_rebuild() -> bool:
     if not os.path.exists(LIB):
         return True

@@ -58,6 +58,12 @@ N_A = 10_000
 ACT_T = 11_000
 T_DISCARD = 1_000
 N_TABLE2 = 24
+# kernel templates the legs' dominant launches are expected to use (PMC entries are matched
+# on them: a template the library no longer launches has no traffic figure)
+C1_PANEL_TEMPLATE = "sim_resident_kernel<512, 8, true, true"
+C3_PANEL_TEMPLATE = "sim_resident_kernel<1024, 4, false, true"
+EGM_C1_TEMPLATE = "egm_cycle_kernel<32, 28, false, 2"
+C4_TEMPLATE = "hist_pull_kernel<32, 512"
 N_TABLE2_CPU_CELL = 6          # (rho 0.6, sigma 0.2, CRRA 1) in stationary.table2_calibrations() order
 
 
@@ -191,7 +197,7 @@ def table2_leg(args, world, rank, dev):
     def sweep():
         return solve_table2(cals, n_a=args.grid, device=dev, method="brent", cu_share=share)
 
-    for _ in range(args.warmup):
+    for _ in range(0 if PMC_PASS else args.warmup):
         sweep()
     hist_stats(h, True, dev)
     ge_stats(h, True, dev)
@@ -222,6 +228,9 @@ def table2_leg(args, world, rank, dev):
         kern = "hist_bicg_kernel (device-resident BiCGSTAB solve of the Young-lottery stationary distribution)"
         hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * point_iters
         s8d_bytes = HIST_BYTES_PER_POINT * point_iters
+    if ge_n > 0:
+        alg_record("table2", "ge_cluster_kernel<7, 7, ", launches=ge_n, alg_bytes=hist_bytes,
+                   note="52 B per point-matvec + 32 B per (state, node) per EGM cycle")
     hist_gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     s8d_gbs = s8d_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
     per_rank = gather_objects(dict(cells=mine, r=[float(x) for x in res.r], KtoY=[float(x) for x in res.KtoY],
@@ -322,7 +331,8 @@ def configs1_leg(args, world, rank, dev):
         finally:
             econ.solve_agents, econ.make_history = solve_agents, make_history
 
-    step()   # warm-up
+    if not PMC_PASS:
+        step()   # warm-up
     for k in stats:
         stats[k] = 0 if isinstance(stats[k], int) else 0.0
     h = _lib.handle(dev.index)
@@ -348,6 +358,13 @@ def configs1_leg(args, world, rank, dev):
     t_egm_ms = egm_kernel_time(agent)
     egm_bytes = 32 * 28 * 15 * (args.grid + 1)
     egm_gbs = egm_bytes / (t_egm_ms * 1e-3) / 1e9
+    alg_record("configs1", C1_PANEL_TEMPLATE, launches=st_n.value, alg_bytes=panel_bytes * st_n.value,
+               units=st_per.value * args.agents, unit_name="agent-period", alg_bytes_per_unit=PANEL_BYTES_PER_AGENT,
+               note="18 B per agent-period")
+    alg_record("configs1", EGM_C1_TEMPLATE, alg_bytes_per_launch=egm_bytes,
+               note="32 B per (state, M node, asset node) per cycle; working launches")
+    p_traffic, p_info = pmc_traffic(C1_PANEL_TEMPLATE, panel_bytes)
+    e_traffic, e_info = pmc_traffic(EGM_C1_TEMPLATE, egm_bytes)
     out = dict(value=world * n_steps / el, unit="GE solves/s", steps=n_steps, seconds=el,
                agent_periods_per_sec=world * n_steps * n_ge * args.act_T * args.agents / el,
                ge_iterations_per_solve=n_ge, egm_cycles_per_ge_iteration=cyc,
@@ -357,14 +374,14 @@ def configs1_leg(args, world, rank, dev):
                        "note": "the reference's market tolerance 0.01 stops this 1M-agent economy after 5 GE "
                                "iterations; at tolerance 1e-4 the same fixed point gives r = 4.092 % "
                                "(profiles/r02a_ks_tolerance_probe.jsonl, DESIGN.md §7)"},
-               roofline={"kernel": "sim_resident_kernel", "bound": "hbm", "achieved": panel_gbs,
+               roofline={"kernel": C1_PANEL_TEMPLATE + ">", "bound": "hbm", "achieved": panel_gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": panel_gbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("sim_resident_kernel"), "algorithmic_bytes_per_launch": panel_bytes,
+                         "traffic": p_traffic, **p_info, "algorithmic_bytes_per_launch": panel_bytes,
                          "avg_launch_ms": t_launch_ms, "us_per_period": 1e3 * t_launch_ms / max(1.0, per_launch),
                          "launch": f"one history: {per_launch:.0f} periods x {args.agents} agents",
                          "launches_timed": st_n.value},
-               roofline_egm={"kernel": "egm_cycle_kernel", "bound": "hbm", "achieved": egm_gbs, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": egm_gbs / HBM_PEAK_GBS, "traffic": pmc_traffic("egm_cycle_kernel"),
+               roofline_egm={"kernel": EGM_C1_TEMPLATE + ">", "bound": "hbm", "achieved": egm_gbs, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": egm_gbs / HBM_PEAK_GBS, "traffic": e_traffic, **e_info,
                              "algorithmic_bytes_per_launch": egm_bytes, "avg_launch_ms": t_egm_ms},
                workload="BASELINE configs[1]: KS-form Aiyagari GE (Aiyagari-HARK.py:249), 28 states x 15 M nodes x "
                         f"{args.grid}-pt grid, {args.agents} agents x {args.act_T} periods per GE iteration, Philox "
@@ -436,8 +453,9 @@ def configs3_leg(args, world, rank, dev):
         comm = bind_rccl(h)[2]
     try:
         p, reset = c3_panel(dev, econ, agent, n_total, T, world, rank)
-        p.run(0, 64, shock_mode="philox", seed=C3_SEED, ge_iter=0, allreduce=allreduce)   # warm-up
-        reset()
+        if not PMC_PASS:
+            p.run(0, 64, shock_mode="philox", seed=C3_SEED, ge_iter=0, allreduce=allreduce)   # warm-up
+            reset()
         h.check(h.lib.aiy_panel_launch_stats(h.h, None, None, None, 1), "stats reset")
         barrier(world)
         t0 = time.perf_counter()
@@ -465,11 +483,17 @@ def configs3_leg(args, world, rank, dev):
                 " + period_price_kernel (wall clock of the periods)")
     bytes_launch = PANEL_BYTES_PER_AGENT * nl * T
     gbs = bytes_launch / max(1e-12, kern_ms * 1e-3) / 1e9
+    traffic, t_info = None, {"traffic_note": "sharded: per-period kernels + all-reduce, not profiled"}
+    if world == 1:
+        alg_record("configs3", C3_PANEL_TEMPLATE, launches=st_n.value, alg_bytes=bytes_launch * max(1, st_n.value),
+                   units=nl * T * max(1, st_n.value), unit_name="agent-period", alg_bytes_per_unit=PANEL_BYTES_PER_AGENT,
+                   note="18 B per agent-period")
+        traffic, t_info = pmc_traffic(C3_PANEL_TEMPLATE, bytes_launch)
     out = dict(value=aps, unit="agent-periods/s", agents=n_total, periods=T, seconds=el, agents_per_rank=nl,
                us_per_period=1e6 * el / T, K_final=float(K_hist[T - 1]), K_first=[float(x) for x in K_hist[:5]],
                roofline={"kernel": kern, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic_periods("sim_resident_kernel_stream", T) if world == 1 else None,
+                         "traffic": traffic, **t_info,
                          "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": kern_ms},
                communicator=comm,
                workload=f"BASELINE configs[3]: {n_total} agents x {T} periods, agents sharded over {world} rank(s), "
@@ -510,9 +534,9 @@ def configs4_leg(args, world, rank, dev):
     def solve():
         return solve_table2(cals, n_a=n_a, device=dev, method="brent", cu_share=share) if cals else None
 
-    solve()   # warm-up
+    if not PMC_PASS:
+        solve()   # warm-up
     hist_stats(h, True, dev)
-    ge_stats(h, True, dev)
     barrier(world)
     t0 = time.perf_counter()
     res = solve()
@@ -523,8 +547,10 @@ def configs4_leg(args, world, rank, dev):
     kern = "hist_pull_kernel<32, 512> (pull-form BiCGSTAB distribution solve, Krylov vectors in HBM)"
     pts = sum(int(np.sum(it)) for it in res.hist_iters) * 25 * n_a if res is not None else 0
     hist_bytes = HIST_BYTES_PER_POINT_KRYLOV * pts
-    trace_name = "hist_pull_kernel"
     gbs = hist_bytes / max(1e-12, hist_ms * 1e-3) / 1e9
+    alg_record("configs4", C4_TEMPLATE, launches=hist_n, alg_bytes=hist_bytes,
+               note="52 B per point-matvec of the pull-form BiCGSTAB solves")
+    traffic, t_info = pmc_traffic(C4_TEMPLATE, hist_bytes / max(1, hist_n))
     per_rank = gather_objects(dict(cells=mine, r=[] if res is None else [float(x) for x in res.r],
                                    status=[] if res is None else [int(x) for x in res.status]), world)
     r = [None] * len(cells)
@@ -537,7 +563,7 @@ def configs4_leg(args, world, rank, dev):
                roofline={"kernel": kern,
                          "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(trace_name + "_c4", scale=None),
+                         "traffic": traffic, **t_info,
                          "algorithmic_bytes_per_launch": hist_bytes / max(1, hist_n),
                          "avg_launch_ms": hist_ms / max(1, hist_n), "launches": hist_n,
                          "kernel_time_share": hist_ms * 1e-3 / max(1e-12, el)},
@@ -570,41 +596,42 @@ def table2_reference_leg(world, rank, dev, agents=350):
                         "one EconomyBatch per rank"}
 
 
-def pmc_traffic_per_sweep(kernel, launches_per_sweep):
-    """HBM bytes per launch of a kernel whose committed PMC passes each profiled ONE sweep
-    (hbm_bytes_total: FETCH x2 + WRITE summed over the sweep's dispatches; the number of
-    rebalancing launches can differ between the two passes), spread over this run's
-    launches per sweep; or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PMC_PASS = False   # --pmc-pass: timed work only, [bench-alg] records for tools/pmc_traffic.py
+
+
+def alg_record(leg, template, **kw):
+    """One [bench-alg] line (stderr) for the PMC passes: the kernel template this leg expects
+    the library to launch and its algorithmic bytes over the leg's launches."""
+    if PMC_PASS:
+        log("[bench-alg] " + json.dumps(dict(leg=leg, template=template, **kw)))
+
+
+def pmc_traffic(template, alg_bytes_per_launch):
+    """HBM traffic per launch of `template` from profiles/pmc_traffic.json (rocprofv3
+    FETCH_SIZE x2 + WRITE_SIZE passes of bench.py --pmc-pass, tools/pmc_traffic.py): the
+    pass's HBM bytes per algorithmic byte of the same launches x this run's algorithmic bytes
+    per launch.  Returns (bytes or None, details): None when no pass profiled this exact
+    template, or when the library's sources changed since the pass (source digest)."""
+    from aiyagari_hark_amd import build
     try:
-        d = json.load(open(path))[kernel]
-        return float(d["hbm_bytes_total"]) / max(1e-9, float(launches_per_sweep))
-    except Exception:
-        return None
-
-
-def pmc_traffic_periods(kernel, periods):
-    """HBM bytes of a launch of `periods` panel periods from the committed PMC passes
-    (hbm_bytes_per_period), or None."""
-    try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[kernel]
-        return float(d["hbm_bytes_per_period"]) * periods
-    except Exception:
-        return None
-
-
-def pmc_traffic(kernel, scale=None):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
-    passes of this bench, FETCH doubled per MI355X_MICROARCH.md), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        d = json.load(open(path))[kernel]
-        if scale is not None and "hbm_bytes_per_point_iter" in d:
-            return float(d["hbm_bytes_per_point_iter"]) * scale
-        return float(d["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+        doc = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    except (OSError, ValueError):
+        return None, {"traffic_note": "profiles/pmc_traffic.json missing"}
+    e = doc.get(template)
+    if e is None:
+        return None, {"traffic_note": f"no PMC pass of {template}"}
+    cur = build.source_digest()
+    if e.get("source_digest") != cur:
+        return None, {"traffic_note": (f"stale: the PMC pass profiled sources {e.get('source_digest')} (head "
+                                       f"{e.get('git_head')}), the library is built from {cur}")}
+    info = {"traffic_hbm_per_alg": e["hbm_per_alg"], "traffic_basis": e["basis"],
+            "traffic_pass": {"git_head": e["git_head"], "source_digest": e["source_digest"],
+                             "kernels": e["kernels"], "dispatches": e["dispatches"],
+                             "hbm_bytes_per_launch_profiled": e["hbm_bytes_per_launch"]}}
+    if "hbm_bytes_per_unit" in e:
+        info["traffic_per_unit"] = {"unit": e.get("unit_name"), "hbm_bytes": e["hbm_bytes_per_unit"],
+                                    "algorithmic_bytes": e.get("alg_bytes_per_unit")}
+    return e["hbm_per_alg"] * alg_bytes_per_launch, info
 
 
 # ------------------------------------------------------------------------------------
@@ -726,6 +753,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: one-GPU rehearsal of the multi-rank run (every rank on device 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-pass", action="store_true",
+                    help="profiling pass (tools/prof_bench.sh): timed work only, [bench-alg] records on stderr")
     ap.add_argument("--hist-pull", type=int, default=None,
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     ap.add_argument("--ge-rebalance", type=int, default=None,
@@ -733,6 +762,8 @@ def main():
     ap.add_argument("--ge-loose-hist", type=int, default=None,
                     help="AIY_OPT_GE_LOOSE_HIST (loose-bracketing histogram tolerance 10^-v; default the library's)")
     args = ap.parse_args()
+    global PMC_PASS
+    PMC_PASS = args.pmc_pass
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)
 
@@ -758,6 +789,8 @@ def main():
         _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]
+    t2_traffic, t2_info = (pmc_traffic("ge_cluster_kernel<7, 7, ", t2["hist_bytes_per_launch"]) if t2["resident"] else
+                           (None, {"traffic_note": "host-driven loop: not profiled"}))
     line = {
         "metric": "GE solves/sec (Table II sweep); agent-periods/sec; % HBM roofline",
         "value": t2["value"],
@@ -782,18 +815,15 @@ def main():
         "roofline": {"kernel": t2["kernel"], "bound": "hbm",
                      "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
-                     "traffic": (pmc_traffic_per_sweep("ge_cluster_kernel", t2["hist_launches_per_sweep"])
-                                 if t2["resident"] else
-                                 pmc_traffic("hist_bicg_kernel",
-                                             scale=t2["hist_bytes_per_launch"] / HIST_BYTES_PER_POINT_KRYLOV)),
+                     "traffic": t2_traffic, **t2_info,
                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
                      "avg_launch_ms": t2["hist_avg_launch_ms"],
                      "launch": ("one launch of the device-resident search (a sweep of the rank's calibrations "
                                 "runs as a few rebalancing launches, every K_s(r) evaluation of every root search "
                                 "in one of them): 52 B per state x node point per matvec of the distribution "
                                 "solves (28 B lottery push + mix, 24 B iterate updates) + 32 B per state x node "
-                                "per EGM cycle; traffic: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of the "
-                                "same sweep" if t2["resident"] else
+                                "per EGM cycle; traffic: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a profiled sweep "
+                                "per algorithmic byte, times this run's algorithmic bytes per launch" if t2["resident"] else
                                 "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
                                 "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
                                 "updates)"),

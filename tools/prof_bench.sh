@@ -1,30 +1,33 @@
 #!/bin/bash
 # Profiles of the bench command (run on the GPU box from the repo root), one stage per
-# call -- rocprofv3 --pmc runs end with a teardown crash of the profiled process after
-# the counters are written, so each PMC pass gets a gpurun call of its own:
-#   trace : rocprofv3 --kernel-trace --stats of one bench step, then the bench line
-#   fetch : --pmc FETCH_SIZE of one bench step
-#   write : --pmc WRITE_SIZE of one bench step
-#   (summary: python3 tools/pmc_traffic.py <fetch> <write> <out.json> <fetch log> [kernels])
-# usage: tools/prof_bench.sh <tag> <stage> [leg]
+# gpurun call (a rocprofv3 --pmc run can end with a teardown crash of the profiled process
+# after the counters are written, so no GPU step may follow it in the same call):
+#   trace : rocprofv3 --kernel-trace --stats of bench.py --pmc-pass (all legs)
+#   fetch : rocprofv3 --pmc FETCH_SIZE of the same command
+#   write : rocprofv3 --pmc WRITE_SIZE of the same command
+# Each stage writes stamp.json (the library's source digest + the git head passed in), so
+# tools/pmc_traffic.py can stamp the traffic it derives with the sources profiled:
+#   python3 tools/pmc_traffic.py $out/pmc_fetch $out/pmc_write $out/pmc_fetch.log $out/stamp.json \
+#       profiles/pmc_traffic.json
+# usage: tools/prof_bench.sh <tag> <stage> <git head> [legs]
 set -o pipefail
-tag=${1:-r01}
+tag=${1:-r06}
 stage=${2:-trace}
+head=${3:-unknown}
+legs=${4:-table2,configs1,configs3,configs4}
 export TMPDIR=/tmp
-out=gpurun_out/bench_$tag
+out=gpurun_out/pmc_$tag
 mkdir -p $out
-leg=${3:-table2}   # bench leg the pass profiles (table2: the headline; configs1: the KS GE solve)
-B="bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs $leg"
-[ "$leg" = table2 ] || out=${out}_$leg
-mkdir -p $out
+python3 -c "import json, sys; sys.path.insert(0, '.'); from aiyagari_hark_amd import build; \
+json.dump({'source_digest': build.source_digest(), 'git_head': '$head'}, open('$out/stamp_$stage.json', 'w'))" || exit 3
+B="bench.py --steps 1 --warmup 0 --no-cpu-baseline --pmc-pass --legs $legs"
 case $stage in
   trace)
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 $B > $out/trace.log 2>&1 || exit 1
-    timeout -k 10 900 python3 bench.py > $out/bench.json 2> $out/bench.err || exit 5 ;;
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 $B > $out/trace.log 2>&1 ;;
   fetch)
-    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $out/pmc_fetch -o run --output-format csv -- python3 $B > $out/pmc_fetch.log 2>&1
-    ls $out/pmc_fetch/*counter_collection.csv ;;
+    timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE -d $out/pmc_fetch -o run --output-format csv -- python3 $B > $out/pmc_fetch.log 2>&1
+    ls $out/pmc_fetch/*/*counter_collection.csv $out/pmc_fetch/*counter_collection.csv 2>/dev/null ;;
   write)
-    timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $out/pmc_write -o run --output-format csv -- python3 $B > $out/pmc_write.log 2>&1
-    ls $out/pmc_write/*counter_collection.csv ;;
+    timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE -d $out/pmc_write -o run --output-format csv -- python3 $B > $out/pmc_write.log 2>&1
+    ls $out/pmc_write/*/*counter_collection.csv $out/pmc_write/*counter_collection.csv 2>/dev/null ;;
 esac
