@@ -52,6 +52,15 @@ constexpr int kGeTHMax = 1024;
 constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
+// One asset column per thread (G >= 20 at N_a = 10 000: every relaunch and the 8-GPU shape):
+// the pipelined BiCGSTAB (hist_bicg.h), one cluster synchronisation per matvec.  Two columns
+// per thread keep the standard recurrence (its vectors would not fit registers + LDS).
+// A diagnostic build with -DAIY_DIAG_NO_PIPE runs the standard form everywhere (A/B timing).
+#ifdef AIY_DIAG_NO_PIPE
+constexpr bool kGePipe = false;
+#else
+constexpr bool kGePipe = true;
+#endif
 template <int NW>
 constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
 
@@ -746,7 +755,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.Qg = to_global(g.qb + row0);
       hk.Ainv = to_global(g.ainv + (size_t)cal * S * (n_a + 1));
       hk.lottery_fresh = true;
-      mv = g.pull ? hk_solve_inlined<SMAX, KC, TH, true>(hk, &nb, &ne) : hk_solve_isolated<SMAX, KC, TH, false>(hk, &nb, &ne);
+      mv = g.pull ? hk_solve_inlined<SMAX, KC, TH, true>(hk, &nb, &ne)
+                  : hk_solve_isolated<SMAX, KC, TH, false, KC == 1 && kGePipe>(hk, &nb, &ne);
     }
     if (mv == -1) return;
     if (tid == 0) {
@@ -879,7 +889,9 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   const size_t stat = fa.sharedSizeBytes;
   if (stat + 4096 >= lds_total) return false;
   p.lds = (lds_total - stat - 1024) / 256 * 256;
-  const size_t vbytes = (size_t)p.kc * p.smax * th * sizeof(double);   // BiCGSTAB v behind the spans
+  // BiCGSTAB v behind the spans; the pipelined form (one column per thread) also x and p
+  const int nvec = (p.kc == 1 && kGePipe && !h->hist_pull) ? kHkPipeLdsVecs : 1;
+  const size_t vbytes = (size_t)nvec * p.kc * p.smax * th * sizeof(double);
   const size_t egm_lds = ge_egm_lds<8>();
   if (p.lds < egm_lds || p.lds <= vbytes + 4096) return false;
   p.cap = (int)((p.lds - vbytes) / sizeof(double));

@@ -13,6 +13,31 @@ constexpr int kHkRed = 8;   // partial sums per reduction (at most)
 constexpr int kHkStall = 256;   // matvecs without a 10 % residual gain that count as a stall
 constexpr double kHkStopSentinel = 1e300;   // rebalancing stop request on the max|r| partial
 static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
+// Destinations covered by more than two spans (the borrowing constraint, the top of the grid:
+// up to kHcCand covering workgroups) are summed by a whole wave, one candidate per lane, instead
+// of a serial per-lane loop whose dependent slab loads put the owning workgroup ~2 us behind the
+// others every matvec (tools/hist_phases.py at G = 32: its gather 4.2 vs 1.6-2.4 us).  Up to
+// kHkHeavy such (column, state) entries per workgroup; more fall back to the per-lane loop.
+constexpr int kHkHeavy = 31;
+constexpr int kHkPipeLdsVecs = 4;   // pipelined BiCGSTAB: v, x, p, s in LDS behind the spans
+static_assert(kHcCand <= 32, "covering-span index and count packed in 5 + 6 bits");
+// covering info of one (column, state): first candidate (5 bits), count (6 bits), heavy-entry
+// index (5 bits; kHkHeavy = none)
+__device__ __forceinline__ unsigned short hk_cinfo(int cf, int cn, int hi) {
+  return (unsigned short)(cf | (cn << 5) | (hi << 11));
+}
+__device__ __forceinline__ int hk_cf(int ci) { return ci & 31; }
+__device__ __forceinline__ int hk_cn(int ci) { return (ci >> 5) & 63; }
+__device__ __forceinline__ int hk_hi(int ci) { return ci >> 11; }
+
+// a wave-uniform double kept in SGPRs (the solve's scalars: otherwise VGPR pairs that the
+// pipelined form spilled to scratch inside its loop)
+__device__ __forceinline__ double hk_uni(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 // shadow residual: a fixed pseudo-random value in [-1, 1) per point index q = s n_a + j
 __device__ __forceinline__ double hk_rhat(unsigned q) {
@@ -59,6 +84,10 @@ struct HkShared {
   int* s_flag;
   int* s_stop;
   int* s_ex;                       // [SMAX][2] pull form: exported prefix / suffix of the own sources
+  int* s_nheavy;                   // heavy (column, state) entries of this workgroup
+  int (*s_heavy)[4];               // [kHkHeavy] (k, s, tid, cf | cn << 8)
+  double* s_hval;                  // [kHkHeavy] their wave sums
+  int* s_rok;                      // reduction riding on a matvec barrier: granules read in time
 };
 
 // One calibration's BiCGSTAB distribution solve by the workgroups of its cluster (this
@@ -97,7 +126,7 @@ struct HkArgs {
 // a rebalancing stop was requested (X holds the current iterate; a later solve restarts
 // from it).  nb / ne: the
 // cluster barriers / reductions passed so far in this launch (counted on).
-template <int SMAX, int KC, int TH, bool PULL = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
 __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
                                         unsigned& ne) {
   constexpr bool kVlds = SMAX <= 8;
@@ -227,6 +256,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       tot += ll;
     }
     s_tot = tot;
+    *L.s_nheavy = 0;
     if (tot > cap) bad = 2u;
     if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -280,12 +310,28 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           }
         }
       }
-      s_cinfo[(k * SMAX + s) * TH + tid] = (unsigned short)(cf | (cn << 8));
+      int hi = kHkHeavy;
+      if (cn > 2) {   // a heavy destination: a wave-parallel entry (order of entries immaterial)
+        const int e = atomicAdd(L.s_nheavy, 1);
+        if (e < kHkHeavy) {
+          hi = e;
+          L.s_heavy[e][0] = k;
+          L.s_heavy[e][1] = s;
+          L.s_heavy[e][2] = tid;
+          L.s_heavy[e][3] = cf | (cn << 8);
+        }
+      }
+      s_cinfo[(k * SMAX + s) * TH + tid] = hk_cinfo(cf, cn, hi);
     }
   }
   // lottery in registers with one column per thread at <= 8 waves (256 VGPRs); with two columns
   // per thread, or 16 waves (128 VGPRs), the registers hold the Krylov vectors
-  constexpr bool kLoReg = SMAX <= 8 && KC == 1 && TH <= 512;
+  // (not in the pipelined form: its six register vectors leave no room, the lottery is re-read
+  // from L2 in each push instead -- with it in registers the solve spilled 196 B per lane)
+#ifndef AIY_PIPE_LOREG
+#define AIY_PIPE_LOREG 0
+#endif
+  constexpr bool kLoReg = SMAX <= 8 && KC == 1 && TH <= 512 && (!PIPE || AIY_PIPE_LOREG);
   int dreg[KC][kLoReg ? SMAX : 1];
   double wreg[KC][kLoReg ? SMAX : 1];
   if constexpr (kLoReg) {
@@ -410,7 +456,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
             v1[k][q] = 0.0;
             oq[k][q] = -1;
             if (s < S) {
-              const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+              const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = hk_cf(ci), cn = hk_cn(ci);
               if (cn >= 1) {
                 const HcCand c = s_cand[s][cf];
                 if (c.w != w) v0[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
@@ -421,7 +467,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
                 if (c.w != w) v1[k][q] = load_f64_agent(&slab_cl[((size_t)c.w * 2 + par) * cap + c.base + d]);
                 else oq[k][q] = c.base + d;
               }
-              more = more || cn > 2;
+              more = more || (cn > 2 && hk_hi(ci) == kHkHeavy);
             }
           }
         }
@@ -439,14 +485,50 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           for (int q = 0; q < GR; ++q) T[k][s0 + q] = (v0[k][q] + v1[k][q]) + T[k][s0 + q];
       }
     }
-    if (__any(more)) {   // columns covered by more than two spans (the borrowing constraint)
+    // heavy destinations (more than two covering spans): one wave per entry, candidate 2 + lane
+    // in lane order, summed by the wave's fixed DPP tree; the owner adds the sum
+    const int nh = min(*L.s_nheavy, kHkHeavy);   // block-uniform
+    if (nh > 0) {
+      // every entry of this wave loaded before the first sum (one round trip, not one per entry)
+      constexpr int NW = TH / kWave, EPW = (kHkHeavy + NW - 1) / NW;
+      double hx[EPW];
+#pragma unroll
+      for (int i = 0; i < EPW; ++i) {
+        const int e = wid + i * NW;
+        hx[i] = 0.0;
+        if (e < nh) {   // wave-uniform
+          const int ek = L.s_heavy[e][0], es = L.s_heavy[e][1], et = L.s_heavy[e][2], ec = L.s_heavy[e][3];
+          const int c = 2 + lane;
+          if (c < (ec >> 8)) hx[i] = hc_take(s_cand[es][(ec & 255) + c], w, j0 + et + ek * TH, par, cap, slab_cl, Tacc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EPW; ++i) {
+        const int e = wid + i * NW;
+        if (e < nh) {
+          const double sum = wave_sum_lane63(hx[i]);
+          if (lane == kWave - 1) L.s_hval[e] = sum;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s)
+          if (s < S) {
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid];
+            if (hk_cn(ci) > 2 && hk_hi(ci) < kHkHeavy) T[k][s] += L.s_hval[hk_hi(ci)];
+          }
+    }
+    if (__any(more)) {   // heavy destinations beyond kHkHeavy entries: the per-lane loop
 #pragma unroll
       for (int k = 0; k < KC; ++k) {
         const int d = j0 + tid + k * TH;
 #pragma unroll
         for (int s = 0; s < SMAX; ++s) {
           if (s < S) {
-            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = ci & 255, cn = ci >> 8;
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = hk_cf(ci), cn = hk_cn(ci);
+            if (hk_hi(ci) < kHkHeavy) continue;
             for (int c0 = 2; c0 < cn; c0 += 4) {
               double x[4];
 #pragma unroll
@@ -611,8 +693,8 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   // host zeroes the granules before each launch); slots alternate by epoch parity, and a
   // matvec barrier separates any two reductions, so a slot is rewritten only after every
   // workgroup has read it.
-  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, auto&& prefetch) -> bool {
-    HK_PH(5);
+  // the workgroup's wave partials of nv values into s_part (visible after the next barrier)
+  auto wave_parts = [&](const double* vals, int nv, unsigned kmax) {
 #pragma unroll
     for (int v = 0; v < kHkRed; ++v) {
       if (v < nv) {
@@ -620,10 +702,9 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         if (lane == kWave - 1) s_part[v][wid] = x;
       }
     }
-    __syncthreads();
-    ++ne;
-    const unsigned long long tag = (unsigned long long)ne << 32;
-    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
+  };
+  // threads < nv: the workgroup's values (waves in fixed order) as two tagged granules each
+  auto store_granules = [&](unsigned long long* slot, unsigned long long tag, int nv, unsigned kmax) {
     if (tid < nv) {
       const int v = tid;
       double x = s_part[v][0];
@@ -633,8 +714,11 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       __hip_atomic_store(to_global(g), tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(to_global(g + 1), tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    prefetch();   // loads the step after the reduction needs, in flight across the sweep
-    if (wid == 0) {
+  };
+  // wave 0: every workgroup's granules (until every tag carries this epoch), fixed-order sums
+  // into s_res; *s_ok = 0 on timeout (error word set)
+  auto sweep = [&](const unsigned long long* slot, unsigned long long tag, int nv, unsigned kmax, int* s_ok) {
+    {
       double xa[kHkRed], xb[kHkRed];
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       bool ok;
@@ -664,7 +748,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           break;
         }
       } while (true);
-      if (lane == 0) s_flag = ok ? 1 : 0;
+      if (lane == 0) *s_ok = ok ? 1 : 0;
 #pragma unroll
       for (int v = 0; v < kHkRed; ++v) {
         if (v < nv) {
@@ -674,11 +758,308 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         }
       }
     }
+  };
+  auto reduce = [&](double (&vals)[kHkRed], int nv, unsigned kmax, auto&& prefetch) -> bool {
+    HK_PH(5);
+    wave_parts(vals, nv, kmax);
+    __syncthreads();
+    ++ne;
+    const unsigned long long tag = (unsigned long long)ne << 32;
+    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
+    store_granules(slot, tag, nv, kmax);
+    prefetch();   // loads the step after the reduction needs, in flight across the sweep
+    if (wid == 0) sweep(slot, tag, nv, kmax, &s_flag);
     __syncthreads();
     HK_PH(4);
     return s_flag != 0;
   };
+  // one matvec out = T q whose cluster barrier also carries a reduction of nv values computed
+  // before it (pipelined BiCGSTAB): the granules are stored before the publish's store drain,
+  // so every workgroup's are in memory once the barrier has passed; wave 0 reads them while
+  // the other waves gather, and s_res is valid on return
+  // do_push(): the push of the matvec input (ends with a workgroup barrier)
+  auto matvec_rp = [&](auto&& do_push, double (&out)[KC][SMAX], const double* vals, int nv, unsigned kmax) -> bool {
+    HK_PH(5);
+    wave_parts(vals, nv, kmax);
+    do_push();   // ends with a workgroup barrier: s_part complete
+    HK_PH(0);
+    ++ne;
+    const unsigned long long tag = (unsigned long long)ne << 32;
+    unsigned long long* slot = gran + (size_t)(ne & 1) * G * (2 * kHkRed);
+    store_granules(slot, tag, nv, kmax);
+    const int par = (int)((nb + 1) & 1);
+    publish(par);   // every thread's s_waitcnt vmcnt(0): slabs and granules drained
+    HK_PH(1);
+    if (!barrier()) return false;
+    HK_PH(2);
+    // the sweep by the last wave: with one column per thread its lanes own no columns whenever
+    // a workgroup has <= TH - 64 of them (G >= 23 at N_a = 10 000), so it overlaps the gather
+    if (wid == TH / kWave - 1) sweep(slot, tag, nv, kmax, L.s_rok);
+    gather_mix(par, out);
+    __syncthreads();
+    HK_PH(3);
+    return *L.s_rok != 0;
+  };
+  auto matvec_r = [&](const double (&q)[KC][SMAX], double (&out)[KC][SMAX], const double* vals, int nv,
+                      unsigned kmax) -> bool { return matvec_rp([&] { push(q); }, out, vals, nv, kmax); };
+  // one column per thread: the lottery of the own column loaded ahead of the push (in flight
+  // across the vector updates before it), and the push from those registers
+  auto load_lot = [&](int (&dp)[SMAX], double (&wp)[SMAX]) {
+    const int jc = col();
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      const bool ok = s < S && jc < j1;
+      const int q = min(s, S - 1) * n_a + min(jc, n_a - 1);
+      const int dv = LO[q];
+      const double wv = WL[q];
+      dp[s] = ok ? dv : -1;
+      wp[s] = ok ? wv : 0.0;
+    }
+  };
+  auto push_pre = [&](const double (&q)[KC][SMAX], const int (&dp)[SMAX], const double (&wp)[SMAX]) {
+    const bool act = j0 + tid < j1;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      if (s < S) {   // wave-uniform
+        const int d = dp[s];
+        const double vlo = wp[s] * q[0][s];          // np.add.at(T[s], lo, wlo q)
+        const double vhi = (1.0 - wp[s]) * q[0][s];  // np.add.at(T[s], lo + 1, (1 - wlo) q)
+        const int ilo = __builtin_amdgcn_readlane(v_base, s) + d, ihi = ilo + 1;
+        const int d0 = __builtin_amdgcn_readfirstlane(d);
+        if (__all(act && d == d0)) {   // the whole wave on one destination (borrowing constraint)
+          const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
+          if (lane == kWave - 1) {
+            atomicAdd(&Tacc[ilo], tl);
+            if (th != 0.0) atomicAdd(&Tacc[ihi], th);
+          }
+        } else if (act) {
+          if (vlo != 0.0) atomicAdd(&Tacc[ilo], vlo);
+          if (vhi != 0.0) atomicAdd(&Tacc[ihi], vhi);
+        }
+      }
+    }
+    __syncthreads();
+  };
 
+  // ---- pipelined BiCGSTAB (Cools & Vanroose's p-BiCGStab, one column per thread) ----
+  // With A = I - T and the auxiliary vectors w = A r, s = A p, z = A s, t = A w, v = A z kept by
+  // recurrences, each iteration's two reductions are formed from vectors known BEFORE its two
+  // matvecs and ride on their cluster barriers (matvec_r): one cluster synchronisation per
+  // matvec instead of two.
+  //   p = r + beta (p - omega s);  s = w + beta (s - omega z);  z = t + beta (z - omega v)
+  //   q = r - alpha s;  y = w - alpha z          R1: <q, y>, <y, y>, <rh, s>, <rh, z>, max|q|
+  //   v = A z                                    (R1 rides on this matvec)
+  //   omega = <q, y> / <y, y>;  x += alpha p + omega q;  r = q - omega y;  w = y - omega (t - alpha v)
+  //                                              R2: <rh, r>, <rh, w>, max|r|
+  //   t = A w                                    (R2 rides on this matvec)
+  //   beta = (alpha / omega) (<rh, r> / rho);  rho = <rh, r>
+  //   alpha = rho / (<rh, w> + beta <rh, s> - beta omega <rh, z>)
+  // The stopping rule and the restart (true residual, T x returned for an x with
+  // max|T x - x| < tol) are the standard form's.  Registers: r, w, t, z, q, y (one column x
+  // SMAX states each); LDS behind the spans: v, x, p and s.
+  if constexpr (PIPE) {
+    static_assert(KC == 1 && !PULL && SMAX <= 8, "pipelined BiCGSTAB: push form, one column per thread");
+    double* Vp = Tacc + cap;
+    double* Xl = Vp + SMAX * TH;
+    double* Pl = Xl + SMAX * TH;
+    double* Sl = Pl + SMAX * TH;
+    auto li = [&](int s) { return s * TH + tid; };
+    double rv[1][SMAX], wv[1][SMAX], tv[1][SMAX], zv[1][SMAX], qv[1][SMAX], yv[1][SMAX];
+    double part[kHkRed];
+    const double tol = r.tol;
+    int mv = 0;
+    bool restart = true, first = true, started = false;
+    double rho = 0.0, alpha = 0.0, beta = 0.0, omega = 0.0, total0 = 0.0, rs = 0.0, rz = 0.0;
+    unsigned seed = 0;
+    double best = __builtin_inf();
+    int mv_best = 0;
+    auto own1 = [&](int jc, int s) { return s < S && jc < j1; };
+    auto rh1 = [&](int jc, int s) { return hk_rhat((unsigned)(s * n_a + jc) + seed * 0x5BD1E995u); };
+    {   // x of the own points into LDS
+      const int jc = col();
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const double xv = X[min(s, S - 1) * n_a + min(jc, n_a - 1)];
+        Xl[li(s)] = own1(jc, s) ? xv : 0.0;
+      }
+    }
+    auto store_x = [&](double scale, bool from_tv) {   // the own points of X (from x, or T x in tv)
+      const int jc = col();
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s)
+        if (own1(jc, s)) X[(size_t)s * n_a + jc] = from_tv ? tv[0][s] * scale : Xl[li(s)];
+    };
+    HK_PH(-1);
+    while (true) {
+      if (restart) {
+        // true residual: tv = T x, r = T x - x; then w = A r (carrying <rh, r>, max|r|, sum x)
+        // and t = A w (carrying <rh, w>); alpha = rho / <rh, w>; p = r, s = w, z = t
+        double xt[1][SMAX];
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) xt[0][s] = Xl[li(s)];
+        if (!matvec_r(xt, tv, part, 0, 0u)) return -1;
+        ++mv;
+        int jc = col();
+        double rr = 0.0, rm = 0.0, xs = 0.0;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          rv[0][s] = tv[0][s] - xt[0][s];
+          if (own1(jc, s)) {
+            rr += rh1(jc, s) * rv[0][s];
+            rm = nan_max(rm, fabs(rv[0][s]));
+            xs += xt[0][s];
+          }
+        }
+        part[0] = rr;
+        part[1] = rm;
+        part[2] = xs;
+        if (!matvec_r(rv, wv, part, 3, 2u)) return -1;
+        ++mv;
+        rho = hk_uni(s_res[0]);
+        if (!started) total0 = hk_uni(s_res[2]);   // the starting mass's total
+        if (s_res[1] < tol || mv >= r.max_iter) {   // converged (NaN never is): T x, rescaled
+          // T x rescaled to the start's total (T preserves totals; near a breakdown rounding can
+          // move sum(x)); the very first check returns T x of the start itself
+          store_x(started ? total0 / s_res[2] : 1.0, true);
+          break;
+        }
+        started = true;
+        jc = col();
+        double rw = 0.0;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          wv[0][s] = rv[0][s] - wv[0][s];
+          if (own1(jc, s)) rw += rh1(jc, s) * wv[0][s];
+        }
+        part[0] = rw;
+        if (!matvec_r(wv, tv, part, 1, 0u)) return -1;
+        ++mv;
+        alpha = hk_uni(rho / s_res[0]);
+        if (!(fabs(alpha) < 1e300) || rho == 0.0) {   // <rh, w> = 0: the next shadow residual
+          ++seed;
+          continue;
+        }
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          tv[0][s] = wv[0][s] - tv[0][s];
+          Pl[li(s)] = rv[0][s];
+          Sl[li(s)] = wv[0][s];
+          zv[0][s] = tv[0][s];
+        }
+        restart = false;
+        first = true;
+        best = __builtin_inf();
+        mv_best = mv;
+      }
+      int dl[SMAX];
+      double wl[SMAX];
+      load_lot(dl, wl);   // in flight across the updates below
+      if (!first) {
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          const double pold = Pl[li(s)], sold = Sl[li(s)];
+          Pl[li(s)] = rv[0][s] + beta * (pold - omega * sold);
+          Sl[li(s)] = wv[0][s] + beta * (sold - omega * zv[0][s]);
+          zv[0][s] = tv[0][s] + beta * (zv[0][s] - omega * Vp[li(s)]);
+        }
+      }
+      // rebalancing stop request: polled every 8th iteration (mv >> 1: iterations) by thread 0;
+      // it rides on the max|q| partial as a sentinel (the cluster max is the same everywhere)
+      if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
+        s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
+      int jc = col();
+      double qy = 0.0, yy = 0.0, hs = 0.0, hz = 0.0, qm = 0.0;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const double sl = Sl[li(s)];
+        qv[0][s] = rv[0][s] - alpha * sl;
+        yv[0][s] = wv[0][s] - alpha * zv[0][s];
+        if (own1(jc, s)) {
+          const double h = rh1(jc, s);
+          qy += qv[0][s] * yv[0][s];
+          yy += yv[0][s] * yv[0][s];
+          hs += h * sl;
+          hz += h * zv[0][s];
+          qm = nan_max(qm, fabs(qv[0][s]));
+        }
+      }
+      part[0] = qy;
+      part[1] = yy;
+      part[2] = hs;
+      part[3] = hz;
+      part[4] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : qm;
+      double zt[1][SMAX];   // T z
+      if (!matvec_rp([&] { push_pre(zv, dl, wl); }, zt, part, 5, 16u)) return -1;
+      ++mv;
+      if (s_res[4] >= kHkStopSentinel) {   // every workgroup reads the same max
+        store_x(1.0, false);
+        return -(2 + mv);
+      }
+      omega = hk_uni((s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1]);
+      if (!(fabs(omega) < 1e300)) omega = 0.0;
+      rs = hk_uni(s_res[2]);
+      rz = hk_uni(s_res[3]);
+      if (omega == 0.0) {   // q already below tol (x + alpha p is the answer), or <y, y> = 0: verify
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) Xl[li(s)] += alpha * Pl[li(s)];
+        restart = true;
+        continue;
+      }
+      load_lot(dl, wl);
+      jc = col();
+      double hr = 0.0, hw = 0.0, rm = 0.0;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const double vz = zv[0][s] - zt[0][s];
+        Vp[li(s)] = vz;
+        Xl[li(s)] = Xl[li(s)] + alpha * Pl[li(s)] + omega * qv[0][s];
+        rv[0][s] = qv[0][s] - omega * yv[0][s];
+        wv[0][s] = yv[0][s] - omega * (tv[0][s] - alpha * vz);
+        if (own1(jc, s)) {
+          const double h = rh1(jc, s);
+          hr += h * rv[0][s];
+          hw += h * wv[0][s];
+          rm = nan_max(rm, fabs(rv[0][s]));
+        }
+      }
+      part[0] = hr;
+      part[1] = hw;
+      part[2] = rm;
+      if (!matvec_rp([&] { push_pre(wv, dl, wl); }, tv, part, 3, 4u)) return -1;
+      ++mv;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) tv[0][s] = wv[0][s] - tv[0][s];
+      if (s_res[2] < tol || mv >= r.max_iter) {   // recursive residual converged: verify
+        restart = true;
+        continue;
+      }
+      // stagnation: no 10 % gain in kHkStall matvecs -> restart with the next shadow residual
+      const double rmax = hk_uni(s_res[2]);
+      if (first || rmax < 0.9 * best) {
+        best = rmax;
+        mv_best = mv;
+      } else if (mv - mv_best > kHkStall) {
+        ++seed;
+        restart = true;
+        continue;
+      }
+      first = false;
+      const double rho2 = hk_uni(s_res[0]);
+      beta = hk_uni((alpha / omega) * (rho2 / rho));
+      const double den = s_res[1] + beta * rs - beta * omega * rz;
+      alpha = hk_uni(rho2 / den);
+      rho = rho2;
+      if (!(fabs(beta) < 1e300) || !(fabs(alpha) < 1e300) || rho == 0.0) restart = true;
+    }
+#ifdef AIY_DIAG_PHASES
+    if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10 && mv > 0)
+      printf("[bicg phases] block %d G=%d nj=%d matvecs=%d us/matvec: push %.2f publish %.2f barrier %.2f gather+mix "
+             "%.2f reduce %.2f vector %.2f\n",
+             (int)blockIdx.x, G, j1 - j0, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv,
+             ph[3] * 0.01 / mv, ph[4] * 0.01 / mv, ph[5] * 0.01 / mv);
+#endif
+    return mv;
+  }
   // ---- BiCGSTAB ----
   // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
   // p in the HBM scratch row across the second matvec, whose gather needs the registers
@@ -901,10 +1282,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 // carries a lot of live state of its own (ge_resident.hip's search loop) would otherwise
 // force the solve's registers into scratch; the call costs a few register saves per
 // solve.  The span buffer / v share the caller's dynamic LDS.
-template <int SMAX, int KC, int TH, bool PULL = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io);
 // the same body inlined into the caller (the pull form spilled more as a separate function)
-template <int SMAX, int KC, int TH, bool PULL = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
 __device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn_in[];
   __shared__ int s_base[SMAX];
@@ -918,15 +1299,17 @@ __device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsig
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  const HkShared<SMAX, KC, TH> L{hk_dyn_in, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex};
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ double s_hval[kHkHeavy];
+  HkShared<SMAX, KC, TH> L{hk_dyn_in, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH, PULL>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL, PIPE>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;
 }
-template <int SMAX, int KC, int TH, bool PULL>
+template <int SMAX, int KC, int TH, bool PULL, bool PIPE>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn[];
   __shared__ int s_base[SMAX];
@@ -940,10 +1323,12 @@ __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigne
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  const HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex};
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ double s_hval[kHkHeavy];
+  HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH, PULL>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL, PIPE>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;

@@ -48,14 +48,16 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   __shared__ int s_tot;
   __shared__ HcCand s_cand[SMAX][kHcCand];
   __shared__ int s_ncand[SMAX];
-  __shared__ unsigned short s_cinfo[KC * SMAX * TH];   // cf | cn << 8 (cf, cn <= kHcCand): LDS for 25 states
+  __shared__ unsigned short s_cinfo[KC * SMAX * TH];   // hk_cinfo(cf, cn, heavy index)
   __shared__ double s_P[SMAX * SMAX];
   __shared__ double s_part[kHkRed][TH / kWave];
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  const HkShared<SMAX, KC, TH> L{Tacc, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex};
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ double s_hval[kHkHeavy];
+  HkShared<SMAX, KC, TH> L{Tacc, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
   const int G = r.G, S = r.S, n_a = r.n_a;
   const int lc = blockIdx.x / G;
   const int w = blockIdx.x - lc * G;
@@ -155,10 +157,7 @@ const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k, bool pull) {
   }
   if (S == 7 && kc == 2) return *smax_k = 7, hk_fn<7, 2, 512>();
   if (smax == 8) return kc == 1 ? hk_fn<8, 1, 512>() : hk_fn<8, 2, 512>();
-  if (kc != 1) return nullptr;
-  if (smax == 16) return hk_fn<16, 1, 512>();
-  if (S == 25) return *smax_k = 25, hk_fn<25, 1, 512>();
-  return hk_fn<32, 1, 512>();
+  return nullptr;   // S > 8: the pull form (hist_pull_kernel, hc_make_plan)
 }
 
 }  // namespace aiy

@@ -86,6 +86,9 @@ struct aiy_handle {
   hipEvent_t res_ev[2] = {nullptr, nullptr};   // bracket every resident launch (aiy_panel_launch_stats)
   double res_ms_sum = 0.0;
   long long res_launches = 0, res_periods = 0;
+  unsigned res_epoch = 0;            // granule tag base of the next resident launch
+  const void* res_occ_fn = nullptr;  // resident shape whose occupancy was last checked
+  size_t res_occ_lds = 0;
   // block panel: per-calibration markets + seeds (device + pinned staging)
   void* d_blk = nullptr;
   void* h_blk = nullptr;

@@ -297,8 +297,32 @@ extern "C" int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, 
 
   // the persistent kernel simulates the employed sub-states only (Krusell-Smith mode runs
   // the per-period kernel)
-  if (!h->comm && h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P) &&
-      resident_aligned(a, lab)) {
+  const bool res_ok = h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P) &&
+                      resident_aligned(a, lab);
+  // (its Philox pairs (2k, 2k + 1) must not straddle shards: an even agent_offset)
+  if (h->comm && res_ok && (agent_offset & 1) == 0) {
+    // sharded: per period ONE launch of the tuned resident kernel (its streaming form for shards
+    // beyond LDS, e.g. 12.5M agents per rank at configs[3] on 8 GPUs) leaving the shard's sum in
+    // sow[6], the RCCL all-reduce of that double, and the price kernel (mill, AS:1867-1894);
+    // the next period's labour draws ride at the end of each launch
+    // (period t's launch forms period t - 1's prices from the all-reduced sum itself; the price
+    // kernel runs once, after the last all-reduce)
+    hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
+    for (int p = 0; p < n_periods; ++p) {
+      const int fl = kResSharded | (p == 0 ? kResDraw0 : kResPrices | kResKeepTmo) |
+                     (p + 1 < n_periods ? kResDrawNext : 0);
+      rc = launch_resident(h, P, mk, n_local, a, lab, u ? u + (size_t)p * u_ld : nullptr, u_ld, seed, ge_iter, t0 + p,
+                           1, sow, hist_A, hist_M, st, agent_offset, fl, n_total);
+      if (rc) return rc;
+      const ncclResult_t e = ncclAllReduce(sow + 6, sow + 6, 1, ncclDouble, ncclSum, h->comm, st);
+      if (e != ncclSuccess) return fail(h, AIY_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(e));
+    }
+    hipLaunchKernelGGL(period_price_kernel, dim3(1), dim3(64), 0, st, mk, P.mrkv_hist, (long long)n_total, sow,
+                       hist_A, hist_M);
+    AIY_CHECK_LAUNCH(h);
+    return resident_status(h, st, false);
+  }
+  if (!h->comm && res_ok) {
     // one persistent launch for the whole block of periods (panel_resident.hip)
     hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t0);
     rc = launch_resident(h, P, mk, n_local, a, lab, u, u_ld, seed, ge_iter, t0, n_periods, sow, hist_A, hist_M, st);
@@ -365,6 +389,16 @@ extern "C" int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* mo
   r.u_t0 = t; r.emp = emp; r.emp_ld = n_local; r.seed = seed; r.ge_iter = ge_iter; r.sow = sow; r.partials = h->d_partials; r.ticket = h->d_ticket;
   r.hist_A = nullptr; r.hist_M = nullptr; r.finish = 0;
   hipLaunchKernelGGL(set_period_kernel, dim3(1), dim3(64), 0, st, sow, (int)t);
+  if (h->use_resident && !emp && n_local >= kResMinAgents && resident_supported(P) && resident_aligned(a, lab) &&
+      (agent_offset & 1) == 0) {
+    // the tuned resident kernel, one period (its labour draws first), the shard's sum in sow[6]
+    const aiy_market unused{};
+    rc = launch_resident(h, P, unused, n_local, a, lab, u, n_local, seed, ge_iter, t, 1, sow, nullptr, nullptr, st,
+                         agent_offset, kResSharded | kResDraw0);
+    if (rc) return rc;
+    AIY_CHECK_LAUNCH(h);
+    return resident_status(h, st, false);
+  }
   if (n_local > 0) {
     const aiy_market unused{};
     hipLaunchKernelGGL(sim_period_kernel, dim3(sim_blocks(n_local)), dim3(kSimBlock), 0, st, P, r, unused);

@@ -350,11 +350,22 @@ constexpr int kAgents = 2 * kPairs;
 // Host: check the model of one calibration and fill its device view.
 int32_t panel_dev(aiy_handle* h, const aiy_panel_model* model, PanelDev& P);
 
-// Persistent panel (panel_resident.hip), used by aiy_sim_periods on a single rank.
+// Persistent panel (panel_resident.hip), used by aiy_sim_periods.  Single rank: a block of
+// periods in one launch.  Sharded (kResSharded): ONE period per launch whose workgroup 0 leaves
+// the shard's sum of a in sow[6] for the caller's all-reduce and the price kernel (kResDraw0: the
+// launch draws its period's labour states first; kResDrawNext: it draws the next period's after
+// the lookups, as the multi-period launch does while the partial sums travel).
+// kResPrices: the launch first forms period t0 - 1's prices from the all-reduced sum in sow[6]
+// (the mill of the price kernel, by every workgroup; workgroup 0 writes sow and the history)
+// instead of reading them from sow -- one kernel fewer per period.  kResKeepTmo: the timeout
+// word is not re-zeroed (an earlier launch of the same call zeroed it; the host reads it once
+// at the end).
+constexpr int kResSharded = 1, kResDraw0 = 2, kResDrawNext = 4, kResPrices = 8, kResKeepTmo = 16;
 int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, long long n, double* a, uint8_t* lab,
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
-                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st);
-int32_t resident_status(aiy_handle* h, hipStream_t st);
+                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st,
+                        long long offset = 0, int flags = kResDraw0, long long n_total = 0);
+int32_t resident_status(aiy_handle* h, hipStream_t st, bool timed = true);
 bool resident_supported(const PanelDev& P);
 // the persistent kernel moves agent pairs as 16-byte asset / 2-byte labour accesses
 inline bool resident_aligned(const double* a, const uint8_t* lab) {

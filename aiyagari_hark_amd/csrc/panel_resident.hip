@@ -58,6 +58,9 @@ struct ResRun {
   unsigned* tmo;            // timeout word, zeroed
   double* hist_A;
   double* hist_M;
+  unsigned ep0;             // granule tags of period p carry ep0 + p + 1 (unique across launches)
+  long long n_total;        // agents over all ranks (the mill's mean, kResPrices)
+  int flags;                // kResSharded | kResDraw0 | kResDrawNext
 };
 
 __device__ __forceinline__ int draw_labour(const double* s_cdf, int n_lab, int l0, double u) {
@@ -169,14 +172,35 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     }
   }
   if (tid == 0) {
-    s_price[0] = load_f64_agent(&r.sow[0]);
-    s_price[1] = load_f64_agent(&r.sow[3]);
-    s_price[2] = load_f64_agent(&r.sow[4]);
-    s_price[3] = load_f64_agent(&r.sow[2]);
+    if (r.flags & kResPrices) {   // period t0 - 1's mill from the all-reduced sum (AS:1867-1894)
+      const Prices q = calc_prices(mk, P.mrkv_hist[r.t0 - 1], load_f64_agent(&r.sow[6]) / (double)r.n_total);
+      s_price[0] = q.Mnow;
+      s_price[1] = q.Rnow;
+      s_price[2] = q.Wnow;
+      s_price[3] = (double)q.Mrkv;
+      if (blockIdx.x == 0) {   // sow and the history, as period_price_kernel (sow[6] is rewritten only
+        // after every workgroup has read it: at this period's end, behind the granule sweep)
+        store_f64_agent(&r.sow[0], q.Mnow);
+        store_f64_agent(&r.sow[1], q.Aprev);
+        store_f64_agent(&r.sow[2], (double)q.Mrkv);
+        store_f64_agent(&r.sow[3], q.Rnow);
+        store_f64_agent(&r.sow[4], q.Wnow);
+        store_f64_agent(&r.sow[5], 0.0);
+        store_f64_agent(&r.sow[7], (double)r.t0);
+        if (r.hist_A) r.hist_A[r.t0 - 1] = q.Aprev;
+        if (r.hist_M) r.hist_M[r.t0 - 1] = q.Mnow;
+      }
+    } else {
+      s_price[0] = load_f64_agent(&r.sow[0]);
+      s_price[1] = load_f64_agent(&r.sow[3]);
+      s_price[2] = load_f64_agent(&r.sow[4]);
+      s_price[3] = load_f64_agent(&r.sow[2]);
+    }
   }
   __syncthreads();
-  draw_slice<kDrawGroup>(r, L, start, cnt, r.t0, s_cdf, n_lab, tid, TH);
+  if (r.flags & kResDraw0) draw_slice<kDrawGroup>(r, L, start, cnt, r.t0, s_cdf, n_lab, tid, TH);
   __syncthreads();   // period t0's labour draws complete
+  const bool sharded = (r.flags & kResSharded) != 0;
 
   Prices last{};
 #ifdef AIY_DIAG_PHASES
@@ -300,8 +324,8 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     if ((tid & (kWave - 1)) == 0) s_red[tid / kWave] = local;
     __syncthreads();
     AIY_PH(1);
-    const unsigned e = (unsigned)p + 1;
-    unsigned long long* gslot = r.gran + (size_t)(p & 1) * 2 * nb;
+    const unsigned e = r.ep0 + (unsigned)p + 1;
+    unsigned long long* gslot = r.gran + (size_t)(e & 1) * 2 * nb;
     if (tid == 0) {
       double sb = 0.0;
       for (int w = 0; w < nthr / kWave; ++w) sb += s_red[w];
@@ -315,7 +339,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #ifndef AIY_DRAW_MODE
 #define AIY_DRAW_MODE 2
 #endif
-    if (p + 1 < r.n_periods) {
+    if (p + 1 < r.n_periods || (r.flags & kResDrawNext)) {
 #if AIY_DRAW_MODE == 0   // every wave draws, wave 0 then sweeps
       draw_slice<kDrawGroup>(r, L, start, cnt, t + 1, s_cdf, n_lab, tid, TH);
 #elif AIY_DRAW_MODE == 1   // wave 4 takes wave 0's pairs
@@ -329,8 +353,9 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
 #endif
     }
     AIY_PH(2);
-    // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices ----
-    if (tid < kWave) {
+    // ---- 4. wave 0 sweeps every workgroup's granules, sums in fixed order, prices (sharded:
+    //      workgroup 0 leaves the shard's sum for the all-reduce) ----
+    if (tid < kWave && (!sharded || blockIdx.x == 0)) {
       unsigned long long gv[kResGranPerLane];
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       int ok = 1;
@@ -359,7 +384,11 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
-      if (tid == 0) {
+      if (tid == 0 && sharded) {
+        if (!ok) __hip_atomic_store(to_global(r.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_abort = ok ? 0 : 1;
+        store_f64_agent(&r.sow[6], acc);
+      } else if (tid == 0) {
         if (!ok) __hip_atomic_store(to_global(r.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_abort = ok ? 0 : 1;
         last = calc_prices(mk, mrkv_next, acc / (double)r.n);   // np.mean(np.array(aNow))
@@ -374,7 +403,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
       }
     }
     __syncthreads();
-    if (s_abort) return;   // sweep timeout: the host reports it (tmo word)
+    if ((!sharded || blockIdx.x == 0) && s_abort) return;   // sweep timeout: the host reports it (tmo word)
     AIY_PH(4);
   }
   if constexpr (IN_LDS) {
@@ -396,7 +425,7 @@ __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, 
     }
   }
 #endif
-  if (blockIdx.x == 0 && tid == 0 && r.n_periods > 0) {
+  if (blockIdx.x == 0 && tid == 0 && r.n_periods > 0 && !sharded) {
     r.sow[0] = last.Mnow;
     r.sow[1] = last.Aprev;
     r.sow[2] = (double)last.Mrkv;
@@ -460,7 +489,8 @@ static int32_t ensure_res_scratch(aiy_handle* h) {
 // Launch the resident kernel for periods [t0, t0 + n_periods) (single rank).
 int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, long long n, double* a, uint8_t* lab,
                         const double* u, long long u_ld, unsigned long long seed, unsigned ge_iter, int t0,
-                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st) {
+                        int n_periods, double* sow, double* hist_A, double* hist_M, hipStream_t st,
+                        long long offset, int flags, long long n_total) {
   if (!resident_supported(P)) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: header table too large");
   if (!resident_aligned(a, lab))
     return fail(h, AIY_ERR_ARG, "resident panel: assets must be 16-byte and labour states 2-byte aligned");
@@ -498,39 +528,57 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
     attr_set = true;
   }
   ResRun r;
-  r.n = n; r.offset = 0; r.chunk = G.chunk; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld; r.seed = seed;
+  r.n = n; r.offset = offset; r.chunk = G.chunk; r.a = a; r.lab = lab; r.u = u; r.u_ld = u_ld; r.seed = seed;
   r.ge_iter = ge_iter; r.t0 = t0; r.n_periods = n_periods; r.sow = sow;
   r.gran = reinterpret_cast<unsigned long long*>(h->d_res_sync);
   r.tmo = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes);
   r.hist_A = hist_A; r.hist_M = hist_M;
+  r.flags = flags;
+  r.n_total = n_total > 0 ? n_total : n;
+  // granule tags unique over the handle's launches: the slots need zeroing only when the tag
+  // counter starts over (the first launch, or after 2^31 periods)
+  if (h->res_epoch == 0 || h->res_epoch > 0x7fffffffu) {
+    AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
+    h->res_epoch = 0;
+  } else if (!(flags & kResKeepTmo)) {
+    AIY_HIP(h, hipMemsetAsync(reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes, 0, sizeof(unsigned), st));
+  }
+  r.ep0 = h->res_epoch;
+  h->res_epoch += (unsigned)n_periods + 1u;
   PanelDev Pc = P;
   aiy_market mkc = mk;
-  AIY_HIP(h, hipMemsetAsync(h->d_res_sync, 0, kResSyncBytes, st));
   void* args[] = {&Pc, &r, &mkc};
   const void* fn = kernels[sh.id][G.in_lds ? 1 : 0];
   // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
   // against the occupancy query; a plain launch then has the same residency as a
   // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),
   // and the in-kernel sweep is bounded by a wall-clock timeout either way.
-  int per_cu = 0;
-  AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, sh.th, G.lds));
-  if (per_cu < 1) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: workgroup does not fit a CU");
-  AIY_HIP(h, hipEventRecord(h->res_ev[0], st));
+  if (fn != h->res_occ_fn || G.lds != h->res_occ_lds) {   // the occupancy query once per shape
+    int per_cu = 0;
+    AIY_HIP(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, sh.th, G.lds));
+    if (per_cu < 1) return fail(h, AIY_ERR_UNSUPPORTED, "resident panel: workgroup does not fit a CU");
+    h->res_occ_fn = fn;
+    h->res_occ_lds = G.lds;
+  }
+  // HIP events bracket the single-rank launches (aiy_panel_launch_stats); the sharded per-period
+  // launches are timed by the caller's clock
+  const bool timed = !(flags & kResSharded);
+  if (timed) AIY_HIP(h, hipEventRecord(h->res_ev[0], st));
   AIY_HIP(h, hipLaunchKernel(fn, dim3(G.nb), dim3(sh.th), args, G.lds, st));
-  AIY_HIP(h, hipEventRecord(h->res_ev[1], st));
+  if (timed) AIY_HIP(h, hipEventRecord(h->res_ev[1], st));
   h->res_periods += n_periods;
   return AIY_OK;
 }
 
 // Timeout word of the last resident launch (0 = fine).  Synchronises `st`.
-int32_t resident_status(aiy_handle* h, hipStream_t st) {
+int32_t resident_status(aiy_handle* h, hipStream_t st, bool timed) {
   if (!h->d_res_sync) return AIY_OK;
   unsigned tmo = 0;
   AIY_HIP(h, hipMemcpyAsync(&tmo, reinterpret_cast<char*>(h->d_res_sync) + kResGranBytes, sizeof(unsigned),
                             hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipStreamSynchronize(st));
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, h->res_ev[0], h->res_ev[1]) == hipSuccess) {
+  if (timed && hipEventElapsedTime(&ms, h->res_ev[0], h->res_ev[1]) == hipSuccess) {
     h->res_ms_sum += ms;
     h->res_launches += 1;
   }

@@ -22,12 +22,17 @@ from . import _lib
 
 
 def shard_range(n_total: int, world: int, rank: int):
-    """Contiguous, balanced agent range of ``rank``: (offset, n_local)."""
+    """Contiguous, balanced agent range of ``rank``: (offset, n_local), split on agent PAIRS
+    so every offset is even (the Philox draw of a pair (2k, 2k + 1) then never straddles two
+    shards, and the library's resident panel kernel takes every shard)."""
     if not (0 <= rank < world):
         raise ValueError("rank out of range")
-    base, rem = divmod(int(n_total), int(world))
-    n_local = base + (1 if rank < rem else 0)
-    offset = rank * base + min(rank, rem)
+    pairs = (int(n_total) + 1) // 2
+    base, rem = divmod(pairs, int(world))
+    p_off = rank * base + min(rank, rem)
+    p_loc = base + (1 if rank < rem else 0)
+    offset = min(2 * p_off, int(n_total))
+    n_local = max(0, min(2 * (p_off + p_loc), int(n_total)) - offset)
     return offset, n_local
 
 

@@ -218,7 +218,12 @@ int32_t aiy_sim_periods(aiy_handle* h, const aiy_panel_model* model, const aiy_m
  *   -- caller: sow[6] <- sum over ranks of sow[6] --
  *   aiy_sim_period_prices: mill / calc_R_and_W (AS:1839-1894) on sow[6] / n_total; writes
  *                          sow, hist_A[t], hist_M[t] and advances sow[7] to t + 1.
- * Both asynchronous on `stream`. */
+ * Both asynchronous on `stream`, except that aiy_sim_period_local returns after the period
+ * completed when it runs the resident kernel (>= 65536 local agents, even agent_offset, no
+ * employment states).
+ * Sharded aiy_sim_periods (a communicator bound) runs per period the same resident launch
+ * (even agent_offset; parallel.shard_range splits on agent pairs), ncclAllReduce of sow[6]
+ * and the price kernel, and returns after the periods completed. */
 int32_t aiy_sim_period_local(aiy_handle* h, const aiy_panel_model* model, int64_t n_local,
                              int64_t agent_offset, double* a, uint8_t* lab, const double* u,
                              const uint8_t* emp, uint64_t seed, uint32_t ge_iter, int32_t t, double* sow,

@@ -33,7 +33,8 @@ def test_shard_range_partitions():
             assert got[0][0] == 0
             for (o1, n1), (o2, _) in zip(got, got[1:]):
                 assert o1 + n1 == o2
-            assert max(nl for _, nl in got) - min(nl for _, nl in got) <= 1
+            assert all(o % 2 == 0 for o, nl in got if nl)   # Philox pairs never straddle shards
+            assert max(nl for _, nl in got) - min(nl for _, nl in got) <= 3   # one pair + the odd tail
 
 
 def test_split_calibrations_cover():

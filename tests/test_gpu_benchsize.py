@@ -174,8 +174,8 @@ def test_configs3_fullsize_streaming_panel_matches_oracle(c3, gpu):
 
 @pytest.mark.timeout(300)
 def test_configs3_fullsize_two_step_shards_match_oracle(c3, gpu):
-    """The sharded form of configs[3] at full size: two contiguous shards (the second
-    starts at an even global index, 49 999 999), each period aiy_sim_period_local on both
+    """The sharded form of configs[3] at full size: two contiguous shards (split on agent
+    pairs: the second starts at global index 50 000 000), each period aiy_sim_period_local on both
     -> the caller's sum -> aiy_sim_period_prices, against the oracle's history."""
     import ctypes
 

@@ -63,7 +63,6 @@ for step in "$@"; do
     lgnt) for e in 1 0; do run lgnt$e 500 env ENGINE=$e NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=lg11=aiyagari_hark_amd/lib/variants/libaiyagari_lg11.so,lg12=aiyagari_hark_amd/lib/variants/libaiyagari_lg12.so,nt=aiyagari_hark_amd/lib/variants/libaiyagari_nt.so python -u tools/panel_variants.py; done ;;
     sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
-    sub8) run sub8_32 400 python -u tools/table2_rank_subsets.py 8 32 && run sub8_85 400 python -u tools/table2_rank_subsets.py 8 85 ;;
     sub8b) run sub8_16 400 python -u tools/table2_rank_subsets.py 8 16 && run sub8_24 400 python -u tools/table2_rank_subsets.py 8 24 && run sub8_48 400 python -u tools/table2_rank_subsets.py 8 48 ;;
     g3) run g3 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0 ;;
     ring3) run ring3 400 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
@@ -79,6 +78,13 @@ for step in "$@"; do
     bench_t2) run bench_t2 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     trace) export TMPDIR=/tmp; run trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --legs table2 ;;
     trace_c1) export TMPDIR=/tmp; run trace_c1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs1 ;;
+    pipet) run pipet 600 $PYT -s tests/test_gpu_ge_resident.py tests/test_gpu_benchsize.py::test_table2_bench_sweep_matches_oracle_fullsize ;;
+    ab3) for v in default nopipe; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ab3_$v 300 env AIYAGARI_LIB=$lib python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0; done ;;
+    abt2) for v in default nopipe; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abt2_$v 300 env AIYAGARI_LIB=$lib python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline; done ;;
+    sub8) run sub8 400 python -u tools/table2_rank_subsets.py 8 32 ;;
+    ph3) for v in phpipe phstd; do run ph3_$v 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 3 --rebalance 0; done ;;
+    sharded) run sharded 500 $PYT -s tests/test_gpu_sharded.py tests/test_gpu_benchsize.py -k "configs3 or sharded or shard or rccl" ;;
+    c3pred) run c3pred 400 python -u tools/c3_shard_predict.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
