@@ -136,7 +136,8 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   double* d_etol = reinterpret_cast<double*>(base + L.etol);
   double* d_htol = reinterpret_cast<double*>(base + L.htol);
   std::vector<double> etol(n_cal, o->egm_tol), htol(n_cal, o->hist_tol);
-  std::vector<char> loose(n_cal, 0), refine(n_cal, 0);
+  std::vector<char> loose(n_cal, 0), refine(n_cal, 0), adapt(n_cal, 0);
+  std::vector<double> fmin_rel(n_cal, HUGE_VAL);   // smallest accepted |K_s - K_d| / K_d (ge_search.h)
   const bool loose_on = o->loose_bracket && o->method == 1;
   const double kLooseEgm = std::max(o->egm_tol, AIY_GE_LOOSE_EGM), kLooseHist = std::max(o->hist_tol, std::pow(10.0, -(double)h->ge_loose_hist));
   const unsigned sec_blocks = 1024;
@@ -182,6 +183,12 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
         loose[c] = !rs[c].brent && !rs[c].done && !refine[c];
         etol[c] = loose[c] ? kLooseEgm : o->egm_tol;
         htol[c] = loose[c] ? kLooseHist : o->hist_tol;
+        // Brent's evaluations at the adaptive tolerance, refined ones at the full one
+        adapt[c] = 0;
+        if (kGeAdapt && rs[c].brent && !rs[c].done && !refine[c]) {
+          htol[c] = ge_adapt_htol(fmin_rel[c], o->hist_tol, kLooseHist);
+          adapt[c] = htol[c] > o->hist_tol;
+        }
       }
       AIY_HIP(h, hipMemcpyAsync(d_etol, etol.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
       AIY_HIP(h, hipMemcpyAsync(d_htol, htol.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
@@ -257,8 +264,12 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
       r_prev[c] = r_cur[c];
       r_cur[c] = rs[c].x;
       const double f = Ks[c] - Kd[c];
-      refine[c] = loose[c] && !(std::fabs(f) >= kGeSignMargin * Kd[c]);   // NaN: refine
-      if (!refine[c]) rs[c].update(f, Kd[c]);
+      refine[c] = (loose[c] && !(std::fabs(f) >= kGeSignMargin * Kd[c])) ||   // NaN: refine
+                  (adapt[c] && !(std::fabs(f) >= kGeAdaptMargin * htol[c] * Kd[c]));
+      if (!refine[c]) {
+        rs[c].update(f, Kd[c]);
+        fmin_rel[c] = std::min(fmin_rel[c], std::fabs(f) / Kd[c]);
+      }
     }
     ++steps;
   }

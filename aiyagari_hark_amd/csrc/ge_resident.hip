@@ -53,13 +53,13 @@ constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
 // One asset column per thread (G >= 20 at N_a = 10 000: every relaunch and the 8-GPU shape):
-// the pipelined BiCGSTAB (hist_bicg.h), one cluster synchronisation per matvec.  Two columns
-// per thread keep the standard recurrence (its vectors would not fit registers + LDS).
-// A diagnostic build with -DAIY_DIAG_NO_PIPE runs the standard form everywhere (A/B timing).
-#ifdef AIY_DIAG_NO_PIPE
-constexpr bool kGePipe = false;
+// the BiCGSTAB solve's alpha reduction rides on its first matvec's barrier (hist_bicg.h
+// FUSEA), one cluster reduction per iteration instead of two.  A diagnostic build with
+// -DAIY_DIAG_NO_FUSEA runs the plain recurrence everywhere (A/B timing).
+#ifdef AIY_DIAG_NO_FUSEA
+constexpr bool kGeFuseA = false;
 #else
-constexpr bool kGePipe = true;
+constexpr bool kGeFuseA = true;
 #endif
 template <int NW>
 constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
@@ -128,6 +128,8 @@ constexpr int kGeEvRec = 6;
 struct GeState {
   RootSearch rs;
   double R, wage, Kd, etol, htol, theta, r_cur, r_prev, Ks, dist, lam_prev, fext;
+  double fmin;             // smallest |K_s - K_d| / K_d accepted so far (adaptive tolerance)
+  int adapt;               // this evaluation runs at an adaptive histogram tolerance
   int steps, loose, refine, warm_egm, secant, fresh_mass, status, n, stop, nan_stop, moved, extrap;
   int in_hist;             // stopped (rebalancing) inside this evaluation's distribution solve
   int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
@@ -481,6 +483,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st.rs.init(cd.r_lo, cd.r_hi, g.r_tol, g.method, g.loose ? g.logsec : 0);
       st.r_cur = st.r_prev = 0.0;
       st.Ks = 0.0;
+      st.fmin = __builtin_inf();
+      st.adapt = 0;
       st.steps = 0;
       st.refine = 0;
       st.in_hist = 0;
@@ -542,6 +546,12 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
         st.loose = g.loose && g.method == 1 && !st.rs.brent && !st.rs.done && !st.refine;
         st.etol = st.loose ? fmax(g.egm_tol, AIY_GE_LOOSE_EGM) : g.egm_tol;
         st.htol = st.loose ? fmax(g.hist_tol, g.loose_hist) : g.hist_tol;
+        // Brent's evaluations: the adaptive tolerance (ge_search.h), refined ones at the full one
+        st.adapt = 0;
+        if (kGeAdapt && g.loose && g.method == 1 && st.rs.brent && !st.rs.done && !st.refine) {
+          st.htol = ge_adapt_htol(st.fmin, g.hist_tol, fmax(g.hist_tol, g.loose_hist));
+          st.adapt = st.htol > g.hist_tol;
+        }
         st.warm_egm = g.warm_egm && st.steps > 0;
         st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
         st.fresh_mass = !(g.warm_hist && st.steps > 0);
@@ -756,7 +766,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.Ainv = to_global(g.ainv + (size_t)cal * S * (n_a + 1));
       hk.lottery_fresh = true;
       mv = g.pull ? hk_solve_inlined<SMAX, KC, TH, true>(hk, &nb, &ne)
-                  : hk_solve_isolated<SMAX, KC, TH, false, KC == 1 && kGePipe>(hk, &nb, &ne);
+                  : hk_solve_isolated<SMAX, KC, TH, false, KC == 1 && kGeFuseA>(hk, &nb, &ne);
     }
     if (mv == -1) return;
     if (tid == 0) {
@@ -802,8 +812,12 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st.r_prev = st.r_cur;
       st.r_cur = st.rs.x;
       const double f = Ks - st.Kd;
-      st.refine = st.loose && !(fabs(f) >= kGeSignMargin * st.Kd);   // NaN: refine
-      if (!st.refine) st.rs.update(f, st.Kd);
+      st.refine = (st.loose && !(fabs(f) >= kGeSignMargin * st.Kd)) ||   // NaN: refine
+                  (st.adapt && !(fabs(f) >= kGeAdaptMargin * st.htol * st.Kd));
+      if (!st.refine) {
+        st.rs.update(f, st.Kd);
+        st.fmin = fmin(st.fmin, fabs(f) / st.Kd);
+      }
       st.Ks = Ks;
       ++st.steps;
       st.t_k += __builtin_amdgcn_s_memrealtime() - tp;
@@ -889,9 +903,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
   const size_t stat = fa.sharedSizeBytes;
   if (stat + 4096 >= lds_total) return false;
   p.lds = (lds_total - stat - 1024) / 256 * 256;
-  // BiCGSTAB v behind the spans; the pipelined form (one column per thread) also x and p
-  const int nvec = (p.kc == 1 && kGePipe && !h->hist_pull) ? kHkPipeLdsVecs : 1;
-  const size_t vbytes = (size_t)nvec * p.kc * p.smax * th * sizeof(double);
+  const size_t vbytes = (size_t)p.kc * p.smax * th * sizeof(double);   // BiCGSTAB v behind the spans
   const size_t egm_lds = ge_egm_lds<8>();
   if (p.lds < egm_lds || p.lds <= vbytes + 4096) return false;
   p.cap = (int)((p.lds - vbytes) / sizeof(double));

@@ -154,4 +154,24 @@ struct RootSearch {
 // since round 4, 10^-10 before; the full-size Table II / stress parity tests pass at both)
 constexpr double kGeSignMargin = 0.05;
 
+// Adaptive distribution tolerance of Brent's evaluations (with loose bracketing).  A BiCGSTAB
+// solve stopped at max|T x - x| < tol leaves K_s about 4e5 tol off relative (DESIGN.md §4c:
+// 4e-7 at 1e-12), and Brent's next |f| is rarely below 1/100 of the smallest |f| seen so far
+// (the Table II searches: 20-80x per step), so an evaluation at tol = kGeAdaptC |f|_min / K_d
+// already resolves f to well inside its expected size; its sign and value are trusted when
+// |f| >= kGeAdaptMargin tol K_d (5 % at 1e-8, the bracketing margin: 12x the error estimate),
+// else the same r is evaluated again at the full tolerance (continuing from its mass: the
+// stopping rule of the final bracket is unchanged).  -DAIY_DIAG_NO_ADAPT turns it off.
+constexpr double kGeAdaptC = 1e-9;
+constexpr double kGeAdaptMargin = 5e6;
+#ifdef AIY_DIAG_NO_ADAPT
+constexpr bool kGeAdapt = false;
+#else
+constexpr bool kGeAdapt = true;
+#endif
+__host__ __device__ inline double ge_adapt_htol(double fmin_rel, double hist_tol, double loose_hist) {
+  const double t = kGeAdaptC * fmin_rel;
+  return t > loose_hist ? loose_hist : (t < hist_tol ? hist_tol : t);   // NaN: hist_tol
+}
+
 }  // namespace aiy

@@ -19,7 +19,11 @@ static_assert(2 * kHkRed <= kHcRedRec, "two granules per partial sum");
 // others every matvec (tools/hist_phases.py at G = 32: its gather 4.2 vs 1.6-2.4 us).  Up to
 // kHkHeavy such (column, state) entries per workgroup; more fall back to the per-lane loop.
 constexpr int kHkHeavy = 31;
-constexpr int kHkPipeLdsVecs = 4;   // pipelined BiCGSTAB: v, x, p, s in LDS behind the spans
+// only destinations with more than kHkWaveCn covering spans take a wave-parallel entry; the
+// others (3 .. kHkWaveCn spans: the destinations of the lowest workgroup's range that several
+// neighbours' dissaving sources reach, often hundreds of them) load their extra candidates 2
+// and 3 for every state at once, one round trip instead of one per state
+constexpr int kHkWaveCn = 6;
 static_assert(kHcCand <= 32, "covering-span index and count packed in 5 + 6 bits");
 // covering info of one (column, state): first candidate (5 bits), count (6 bits), heavy-entry
 // index (5 bits; kHkHeavy = none)
@@ -126,7 +130,7 @@ struct HkArgs {
 // a rebalancing stop was requested (X holds the current iterate; a later solve restarts
 // from it).  nb / ne: the
 // cluster barriers / reductions passed so far in this launch (counted on).
-template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool FUSEA = false>
 __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC, TH>& L, unsigned& nb,
                                         unsigned& ne) {
   constexpr bool kVlds = SMAX <= 8;
@@ -311,7 +315,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         }
       }
       int hi = kHkHeavy;
-      if (cn > 2) {   // a heavy destination: a wave-parallel entry (order of entries immaterial)
+      if (cn > kHkWaveCn) {   // a heavy destination: a wave-parallel entry (order of entries immaterial)
         const int e = atomicAdd(L.s_nheavy, 1);
         if (e < kHkHeavy) {
           hi = e;
@@ -326,12 +330,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   }
   // lottery in registers with one column per thread at <= 8 waves (256 VGPRs); with two columns
   // per thread, or 16 waves (128 VGPRs), the registers hold the Krylov vectors
-  // (not in the pipelined form: its six register vectors leave no room, the lottery is re-read
-  // from L2 in each push instead -- with it in registers the solve spilled 196 B per lane)
-#ifndef AIY_PIPE_LOREG
-#define AIY_PIPE_LOREG 0
-#endif
-  constexpr bool kLoReg = SMAX <= 8 && KC == 1 && TH <= 512 && (!PIPE || AIY_PIPE_LOREG);
+  constexpr bool kLoReg = SMAX <= 8 && KC == 1 && TH <= 512;
   int dreg[KC][kLoReg ? SMAX : 1];
   double wreg[KC][kLoReg ? SMAX : 1];
   if constexpr (kLoReg) {
@@ -517,19 +516,34 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         for (int s = 0; s < SMAX; ++s)
           if (s < S) {
             const int ci = s_cinfo[(k * SMAX + s) * TH + tid];
-            if (hk_cn(ci) > 2 && hk_hi(ci) < kHkHeavy) T[k][s] += L.s_hval[hk_hi(ci)];
+            if (hk_hi(ci) < kHkHeavy) T[k][s] += L.s_hval[hk_hi(ci)];
           }
     }
-    if (__any(more)) {   // heavy destinations beyond kHkHeavy entries: the per-lane loop
+    if (__any(more)) {   // destinations with more than two covering spans and no wave entry
 #pragma unroll
       for (int k = 0; k < KC; ++k) {
         const int d = j0 + tid + k * TH;
+        double e2[SMAX], e3[SMAX];   // candidates 2 and 3 of every state, all in flight
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          e2[s] = 0.0;
+          e3[s] = 0.0;
+          if (s < S) {
+            const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = hk_cf(ci), cn = hk_cn(ci);
+            if (cn > 2 && hk_hi(ci) == kHkHeavy) {
+              e2[s] = hc_take(s_cand[s][cf + 2], w, d, par, cap, slab_cl, Tacc);
+              if (cn > 3) e3[s] = hc_take(s_cand[s][cf + 3], w, d, par, cap, slab_cl, Tacc);
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) T[k][s] += e2[s] + e3[s];
 #pragma unroll
         for (int s = 0; s < SMAX; ++s) {
           if (s < S) {
             const int ci = s_cinfo[(k * SMAX + s) * TH + tid], cf = hk_cf(ci), cn = hk_cn(ci);
             if (hk_hi(ci) < kHkHeavy) continue;
-            for (int c0 = 2; c0 < cn; c0 += 4) {
+            for (int c0 = 4; c0 < cn; c0 += 4) {   // (more than four spans and no wave entry: rare)
               double x[4];
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
@@ -841,225 +855,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     __syncthreads();
   };
 
-  // ---- pipelined BiCGSTAB (Cools & Vanroose's p-BiCGStab, one column per thread) ----
-  // With A = I - T and the auxiliary vectors w = A r, s = A p, z = A s, t = A w, v = A z kept by
-  // recurrences, each iteration's two reductions are formed from vectors known BEFORE its two
-  // matvecs and ride on their cluster barriers (matvec_r): one cluster synchronisation per
-  // matvec instead of two.
-  //   p = r + beta (p - omega s);  s = w + beta (s - omega z);  z = t + beta (z - omega v)
-  //   q = r - alpha s;  y = w - alpha z          R1: <q, y>, <y, y>, <rh, s>, <rh, z>, max|q|
-  //   v = A z                                    (R1 rides on this matvec)
-  //   omega = <q, y> / <y, y>;  x += alpha p + omega q;  r = q - omega y;  w = y - omega (t - alpha v)
-  //                                              R2: <rh, r>, <rh, w>, max|r|
-  //   t = A w                                    (R2 rides on this matvec)
-  //   beta = (alpha / omega) (<rh, r> / rho);  rho = <rh, r>
-  //   alpha = rho / (<rh, w> + beta <rh, s> - beta omega <rh, z>)
-  // The stopping rule and the restart (true residual, T x returned for an x with
-  // max|T x - x| < tol) are the standard form's.  Registers: r, w, t, z, q, y (one column x
-  // SMAX states each); LDS behind the spans: v, x, p and s.
-  if constexpr (PIPE) {
-    static_assert(KC == 1 && !PULL && SMAX <= 8, "pipelined BiCGSTAB: push form, one column per thread");
-    double* Vp = Tacc + cap;
-    double* Xl = Vp + SMAX * TH;
-    double* Pl = Xl + SMAX * TH;
-    double* Sl = Pl + SMAX * TH;
-    auto li = [&](int s) { return s * TH + tid; };
-    double rv[1][SMAX], wv[1][SMAX], tv[1][SMAX], zv[1][SMAX], qv[1][SMAX], yv[1][SMAX];
-    double part[kHkRed];
-    const double tol = r.tol;
-    int mv = 0;
-    bool restart = true, first = true, started = false;
-    double rho = 0.0, alpha = 0.0, beta = 0.0, omega = 0.0, total0 = 0.0, rs = 0.0, rz = 0.0;
-    unsigned seed = 0;
-    double best = __builtin_inf();
-    int mv_best = 0;
-    auto own1 = [&](int jc, int s) { return s < S && jc < j1; };
-    auto rh1 = [&](int jc, int s) { return hk_rhat((unsigned)(s * n_a + jc) + seed * 0x5BD1E995u); };
-    {   // x of the own points into LDS
-      const int jc = col();
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        const double xv = X[min(s, S - 1) * n_a + min(jc, n_a - 1)];
-        Xl[li(s)] = own1(jc, s) ? xv : 0.0;
-      }
-    }
-    auto store_x = [&](double scale, bool from_tv) {   // the own points of X (from x, or T x in tv)
-      const int jc = col();
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s)
-        if (own1(jc, s)) X[(size_t)s * n_a + jc] = from_tv ? tv[0][s] * scale : Xl[li(s)];
-    };
-    HK_PH(-1);
-    while (true) {
-      if (restart) {
-        // true residual: tv = T x, r = T x - x; then w = A r (carrying <rh, r>, max|r|, sum x)
-        // and t = A w (carrying <rh, w>); alpha = rho / <rh, w>; p = r, s = w, z = t
-        double xt[1][SMAX];
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) xt[0][s] = Xl[li(s)];
-        if (!matvec_r(xt, tv, part, 0, 0u)) return -1;
-        ++mv;
-        int jc = col();
-        double rr = 0.0, rm = 0.0, xs = 0.0;
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-          rv[0][s] = tv[0][s] - xt[0][s];
-          if (own1(jc, s)) {
-            rr += rh1(jc, s) * rv[0][s];
-            rm = nan_max(rm, fabs(rv[0][s]));
-            xs += xt[0][s];
-          }
-        }
-        part[0] = rr;
-        part[1] = rm;
-        part[2] = xs;
-        if (!matvec_r(rv, wv, part, 3, 2u)) return -1;
-        ++mv;
-        rho = hk_uni(s_res[0]);
-        if (!started) total0 = hk_uni(s_res[2]);   // the starting mass's total
-        if (s_res[1] < tol || mv >= r.max_iter) {   // converged (NaN never is): T x, rescaled
-          // T x rescaled to the start's total (T preserves totals; near a breakdown rounding can
-          // move sum(x)); the very first check returns T x of the start itself
-          store_x(started ? total0 / s_res[2] : 1.0, true);
-          break;
-        }
-        started = true;
-        jc = col();
-        double rw = 0.0;
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-          wv[0][s] = rv[0][s] - wv[0][s];
-          if (own1(jc, s)) rw += rh1(jc, s) * wv[0][s];
-        }
-        part[0] = rw;
-        if (!matvec_r(wv, tv, part, 1, 0u)) return -1;
-        ++mv;
-        alpha = hk_uni(rho / s_res[0]);
-        if (!(fabs(alpha) < 1e300) || rho == 0.0) {   // <rh, w> = 0: the next shadow residual
-          ++seed;
-          continue;
-        }
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-          tv[0][s] = wv[0][s] - tv[0][s];
-          Pl[li(s)] = rv[0][s];
-          Sl[li(s)] = wv[0][s];
-          zv[0][s] = tv[0][s];
-        }
-        restart = false;
-        first = true;
-        best = __builtin_inf();
-        mv_best = mv;
-      }
-      int dl[SMAX];
-      double wl[SMAX];
-      load_lot(dl, wl);   // in flight across the updates below
-      if (!first) {
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-          const double pold = Pl[li(s)], sold = Sl[li(s)];
-          Pl[li(s)] = rv[0][s] + beta * (pold - omega * sold);
-          Sl[li(s)] = wv[0][s] + beta * (sold - omega * zv[0][s]);
-          zv[0][s] = tv[0][s] + beta * (zv[0][s] - omega * Vp[li(s)]);
-        }
-      }
-      // rebalancing stop request: polled every 8th iteration (mv >> 1: iterations) by thread 0;
-      // it rides on the max|q| partial as a sentinel (the cluster max is the same everywhere)
-      if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
-        s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
-      int jc = col();
-      double qy = 0.0, yy = 0.0, hs = 0.0, hz = 0.0, qm = 0.0;
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        const double sl = Sl[li(s)];
-        qv[0][s] = rv[0][s] - alpha * sl;
-        yv[0][s] = wv[0][s] - alpha * zv[0][s];
-        if (own1(jc, s)) {
-          const double h = rh1(jc, s);
-          qy += qv[0][s] * yv[0][s];
-          yy += yv[0][s] * yv[0][s];
-          hs += h * sl;
-          hz += h * zv[0][s];
-          qm = nan_max(qm, fabs(qv[0][s]));
-        }
-      }
-      part[0] = qy;
-      part[1] = yy;
-      part[2] = hs;
-      part[3] = hz;
-      part[4] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : qm;
-      double zt[1][SMAX];   // T z
-      if (!matvec_rp([&] { push_pre(zv, dl, wl); }, zt, part, 5, 16u)) return -1;
-      ++mv;
-      if (s_res[4] >= kHkStopSentinel) {   // every workgroup reads the same max
-        store_x(1.0, false);
-        return -(2 + mv);
-      }
-      omega = hk_uni((s_res[4] < tol) ? 0.0 : s_res[0] / s_res[1]);
-      if (!(fabs(omega) < 1e300)) omega = 0.0;
-      rs = hk_uni(s_res[2]);
-      rz = hk_uni(s_res[3]);
-      if (omega == 0.0) {   // q already below tol (x + alpha p is the answer), or <y, y> = 0: verify
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) Xl[li(s)] += alpha * Pl[li(s)];
-        restart = true;
-        continue;
-      }
-      load_lot(dl, wl);
-      jc = col();
-      double hr = 0.0, hw = 0.0, rm = 0.0;
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        const double vz = zv[0][s] - zt[0][s];
-        Vp[li(s)] = vz;
-        Xl[li(s)] = Xl[li(s)] + alpha * Pl[li(s)] + omega * qv[0][s];
-        rv[0][s] = qv[0][s] - omega * yv[0][s];
-        wv[0][s] = yv[0][s] - omega * (tv[0][s] - alpha * vz);
-        if (own1(jc, s)) {
-          const double h = rh1(jc, s);
-          hr += h * rv[0][s];
-          hw += h * wv[0][s];
-          rm = nan_max(rm, fabs(rv[0][s]));
-        }
-      }
-      part[0] = hr;
-      part[1] = hw;
-      part[2] = rm;
-      if (!matvec_rp([&] { push_pre(wv, dl, wl); }, tv, part, 3, 4u)) return -1;
-      ++mv;
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) tv[0][s] = wv[0][s] - tv[0][s];
-      if (s_res[2] < tol || mv >= r.max_iter) {   // recursive residual converged: verify
-        restart = true;
-        continue;
-      }
-      // stagnation: no 10 % gain in kHkStall matvecs -> restart with the next shadow residual
-      const double rmax = hk_uni(s_res[2]);
-      if (first || rmax < 0.9 * best) {
-        best = rmax;
-        mv_best = mv;
-      } else if (mv - mv_best > kHkStall) {
-        ++seed;
-        restart = true;
-        continue;
-      }
-      first = false;
-      const double rho2 = hk_uni(s_res[0]);
-      beta = hk_uni((alpha / omega) * (rho2 / rho));
-      const double den = s_res[1] + beta * rs - beta * omega * rz;
-      alpha = hk_uni(rho2 / den);
-      rho = rho2;
-      if (!(fabs(beta) < 1e300) || !(fabs(alpha) < 1e300) || rho == 0.0) restart = true;
-    }
-#ifdef AIY_DIAG_PHASES
-    if (tid == 0 && blockIdx.x >= AIY_DIAG_PHASES && blockIdx.x < AIY_DIAG_PHASES + 10 && mv > 0)
-      printf("[bicg phases] block %d G=%d nj=%d matvecs=%d us/matvec: push %.2f publish %.2f barrier %.2f gather+mix "
-             "%.2f reduce %.2f vector %.2f\n",
-             (int)blockIdx.x, G, j1 - j0, mv, ph[0] * 0.01 / mv, ph[1] * 0.01 / mv, ph[2] * 0.01 / mv,
-             ph[3] * 0.01 / mv, ph[4] * 0.01 / mv, ph[5] * 0.01 / mv);
-#endif
-    return mv;
-  }
   // ---- BiCGSTAB ----
   // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
   // p in the HBM scratch row across the second matvec, whose gather needs the registers
@@ -1080,6 +875,37 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   double best = __builtin_inf();   // best recursive max|r| since the last restart, and when
   int mv_best = 0;
   auto gidx = [&](int jc, int k, int s) { return (size_t)s * n_a + jc + k * TH; };
+  // FUSEA (one column per thread, the resident search): alpha's reduction rides on the first
+  // matvec's cluster barrier.  <rh, v> = <rh, A p> = <A^T rh, p> with A = I - T, and
+  // u = A^T rh is fixed for a solve (a new shadow residual recomputes it): its own points sit in
+  // the Qg rows, and <u, p> is formed when p is, before the matvec.  One cluster reduction per
+  // iteration instead of two; the same recurrence otherwise.
+  //   (T^T y)[s][j] = sum_s' P[s, s'] (wlo y[s'][lo] + (1 - wlo) y[s'][lo + 1])
+  double* Ug = (double*)r.Qg;
+  double pu = 0.0;   // this thread's part of <u, p>
+  auto make_u = [&]() {   // u of the own points -> Ug; pu = <u, p> with p = r
+    static_assert(!FUSEA || kLoReg, "FUSEA: the lottery of the own column in registers");
+    if constexpr (FUSEA) {
+      const int jc = col();
+      double acc = 0.0;
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        if (own(jc, 0, s)) {
+          const int d = dreg[0][s];
+          const double wl = wreg[0][s];
+          double tr = 0.0;
+          for (int sp = 0; sp < S; ++sp) {
+            const unsigned q = (unsigned)(sp * n_a + d) + seed * 0x5BD1E995u;
+            tr += s_P[s * SMAX + sp] * (wl * hk_rhat(q) + (1.0 - wl) * hk_rhat(q + 1u));
+          }
+          const double u = rh_at(jc, 0, s) - tr;
+          Ug[gidx(jc, 0, s)] = u;
+          acc += u * pv[0][s];
+        }
+      }
+      pu = acc;
+    }
+  };
   HK_PH(-1);
   while (true) {
     if (restart) {
@@ -1129,6 +955,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
       for (int k = 0; k < KC; ++k)
 #pragma unroll
         for (int s = 0; s < SMAX; ++s) pv[k][s] = rv[k][s];
+      make_u();
       restart = false;
       first = true;
     }
@@ -1144,35 +971,58 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     // number is mv >> 1
     if (r.stop_ctr != nullptr && tid == 0 && ((mv >> 1) & 7) == 0)
       s_stop = __hip_atomic_load((const unsigned*)r.stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.stop_at;
-    if (!matvec(pv, tv)) return -1;
-    ++mv;
-    int jc = col();
-    double rvv = 0.0, rm = 0.0;
-#pragma unroll
-    for (int k = 0; k < KC; ++k)
+    double xq[KC][SMAX];   // x of the own points, for x += alpha p
+    int jc;
+    if constexpr (FUSEA) {
+      // <u, p> and max|r| ride on this matvec's barrier (the stop request as a sentinel on the
+      // max, which no residual of a mass vector reaches); x's loads in flight across it
+      jc = col();
+      double rm = 0.0;
 #pragma unroll
       for (int s = 0; s < SMAX; ++s) {
-        const double v = pv[k][s] - tv[k][s];
-        rv[k][s] = Vl[vidx(k, s)];
-        Vl[vidx(k, s)] = v;
-        if (own(jc, k, s)) {
-          rvv += rh_at(jc, k, s) * v;
-          rm = nan_max(rm, fabs(rv[k][s]));
-        }
+        if (own(jc, 0, s)) rm = nan_max(rm, fabs(Vl[vidx(0, s)]));
+        xq[0][s] = X[min(s, S - 1) * n_a + min(jc, n_a - 1)];
       }
-    part[0] = rvv;
-    // the stop request rides on the max|r| partial as a sentinel no residual of a mass vector
-    // reaches (the cluster max is the same in every workgroup)
-    part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
-    double xq[KC][SMAX];   // x of the own points, for x += alpha p
-    if (!reduce(part, 2, 2u, [&] {
-          const int jq = col();
+      part[0] = pu;
+      part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
+      if (!matvec_r(pv, tv, part, 2, 2u)) return -1;
+      ++mv;
 #pragma unroll
-          for (int k = 0; k < KC; ++k)
+      for (int s = 0; s < SMAX; ++s) {
+        const double v = pv[0][s] - tv[0][s];
+        rv[0][s] = Vl[vidx(0, s)];
+        Vl[vidx(0, s)] = v;
+      }
+    } else {
+      if (!matvec(pv, tv)) return -1;
+      ++mv;
+      jc = col();
+      double rvv = 0.0, rm = 0.0;
 #pragma unroll
-            for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
-        }))
-      return -1;
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          const double v = pv[k][s] - tv[k][s];
+          rv[k][s] = Vl[vidx(k, s)];
+          Vl[vidx(k, s)] = v;
+          if (own(jc, k, s)) {
+            rvv += rh_at(jc, k, s) * v;
+            rm = nan_max(rm, fabs(rv[k][s]));
+          }
+        }
+      part[0] = rvv;
+      // the stop request rides on the max|r| partial as a sentinel no residual of a mass vector
+      // reaches (the cluster max is the same in every workgroup)
+      part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
+      if (!reduce(part, 2, 2u, [&] {
+            const int jq = col();
+#pragma unroll
+            for (int k = 0; k < KC; ++k)
+#pragma unroll
+              for (int s = 0; s < SMAX; ++s) xq[k][s] = X[min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1)];
+          }))
+        return -1;
+    }
     if (s_res[1] >= kHkStopSentinel) return -(2 + mv);   // every workgroup reads the same max
     if ((!first && s_res[1] < tol) || mv >= r.max_iter) {   // recursive residual converged: verify
       restart = true;
@@ -1233,6 +1083,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     part[3] = rt;
     part[4] = sm;
     double pq[KC][SMAX];   // x and p of the own points, for x += omega s and the new p
+    double uq[FUSEA ? KC : 1][SMAX];   // FUSEA: u of the own points, for <u, p> of the new p
     if (!reduce(part, 5, 16u, [&] {
           const int jq = col();
 #pragma unroll
@@ -1242,6 +1093,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
               const int g = min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1);
               xq[k][s] = X[g];
               pq[k][s] = Pg[g];
+              if constexpr (FUSEA) uq[k][s] = Ug[g];
             }
         }))
       return -1;
@@ -1256,6 +1108,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     rho = rho2;
     // x += omega s; r = s - omega t; p = r + beta (p - omega v)
     jc = col();
+    double pun = 0.0;
 #pragma unroll
     for (int k = 0; k < KC; ++k)
 #pragma unroll
@@ -1265,7 +1118,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         const double pold = ow ? pq[k][s] : 0.0;
         rv[k][s] = rv[k][s] - omega * tv[k][s];
         pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
+        if constexpr (FUSEA)
+          if (ow) pun += uq[k][s] * pv[k][s];
       }
+    pu = pun;
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }
 #ifdef AIY_DIAG_PHASES
@@ -1282,10 +1138,10 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
 // carries a lot of live state of its own (ge_resident.hip's search loop) would otherwise
 // force the solve's registers into scratch; the call costs a few register saves per
 // solve.  The span buffer / v share the caller's dynamic LDS.
-template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool FUSEA = false>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io);
 // the same body inlined into the caller (the pull form spilled more as a separate function)
-template <int SMAX, int KC, int TH, bool PULL = false, bool PIPE = false>
+template <int SMAX, int KC, int TH, bool PULL = false, bool FUSEA = false>
 __device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn_in[];
   __shared__ int s_base[SMAX];
@@ -1304,12 +1160,12 @@ __device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsig
   HkShared<SMAX, KC, TH> L{hk_dyn_in, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
                                  &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH, PULL, PIPE>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL, FUSEA>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;
 }
-template <int SMAX, int KC, int TH, bool PULL, bool PIPE>
+template <int SMAX, int KC, int TH, bool PULL, bool FUSEA>
 __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigned* ne_io) {
   extern __shared__ double hk_dyn[];
   __shared__ int s_base[SMAX];
@@ -1328,7 +1184,7 @@ __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigne
   HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
                                  &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hk_solve<SMAX, KC, TH, PULL, PIPE>(a, L, nb, ne);
+  const int mv = hk_solve<SMAX, KC, TH, PULL, FUSEA>(a, L, nb, ne);
   *nb_io = nb;
   *ne_io = ne;
   return mv;

@@ -79,12 +79,13 @@ for step in "$@"; do
     trace) export TMPDIR=/tmp; run trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --legs table2 ;;
     trace_c1) export TMPDIR=/tmp; run trace_c1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs1 ;;
     pipet) run pipet 600 $PYT -s tests/test_gpu_ge_resident.py tests/test_gpu_benchsize.py::test_table2_bench_sweep_matches_oracle_fullsize ;;
-    ab3) for v in default nopipe; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ab3_$v 300 env AIYAGARI_LIB=$lib python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0; done ;;
-    abt2) for v in default nopipe; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abt2_$v 300 env AIYAGARI_LIB=$lib python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline; done ;;
+    ab3) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ab3_$v 300 env AIYAGARI_LIB=$lib python -u tools/ge_resident_profile.py --modes resident --reps 3 --cells 3 --rebalance 0; done ;;
+    abt2) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abt2_$v 300 env AIYAGARI_LIB=$lib python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline; done ;;
     sub8) run sub8 400 python -u tools/table2_rank_subsets.py 8 32 ;;
-    ph3) for v in phpipe phstd; do run ph3_$v 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 3 --rebalance 0; done ;;
+    ph3) for v in ${PHVARIANTS:-phfusea}; do run ph3_$v 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 3 --rebalance 0; done ;;
     sharded) run sharded 500 $PYT -s tests/test_gpu_sharded.py tests/test_gpu_benchsize.py -k "configs3 or sharded or shard or rccl" ;;
     c3pred) run c3pred 400 python -u tools/c3_shard_predict.py ;;
+    abc4) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abc4_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs configs4 --steps 1 --warmup 0 --no-cpu-baseline; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
