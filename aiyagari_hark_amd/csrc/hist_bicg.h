@@ -22,8 +22,12 @@ constexpr int kHkHeavy = 31;
 // only destinations with more than kHkWaveCn covering spans take a wave-parallel entry; the
 // others (3 .. kHkWaveCn spans: the destinations of the lowest workgroup's range that several
 // neighbours' dissaving sources reach, often hundreds of them) load their extra candidates 2
-// and 3 for every state at once, one round trip instead of one per state
-constexpr int kHkWaveCn = 6;
+// and 3 for every state at once, one round trip instead of one per state (Table II sweep
+// 60.5 -> 57.9 ms against kHkWaveCn = 2, gpurun_out r07a abt2)
+#ifndef AIY_HK_WAVE_CN
+#define AIY_HK_WAVE_CN 6
+#endif
+constexpr int kHkWaveCn = AIY_HK_WAVE_CN;
 static_assert(kHcCand <= 32, "covering-span index and count packed in 5 + 6 bits");
 // covering info of one (column, state): first candidate (5 bits), count (6 bits), heavy-entry
 // index (5 bits; kHkHeavy = none)
@@ -89,6 +93,7 @@ struct HkShared {
   int* s_stop;
   int* s_ex;                       // [SMAX][2] pull form: exported prefix / suffix of the own sources
   int* s_nheavy;                   // heavy (column, state) entries of this workgroup
+  int* s_wcnt;                     // [TH / kWave] per-wave counts while numbering them
   int (*s_heavy)[4];               // [kHkHeavy] (k, s, tid, cf | cn << 8)
   double* s_hval;                  // [kHkHeavy] their wave sums
   int* s_rok;                      // reduction riding on a matvec barrier: granules read in time
@@ -314,17 +319,28 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
           }
         }
       }
+      // a heavy destination: a wave-parallel entry, numbered in (k, s, thread) order so that
+      // which destinations get the kHkHeavy entries (and so the summation order of the
+      // others) is the same in every run
+      const bool heavy = cn > kHkWaveCn;
+      const unsigned long long bm = __ballot(heavy);
+      if (lane == 0) L.s_wcnt[wid] = __popcll(bm);
+      __syncthreads();
+      int base = *L.s_nheavy;
+      for (int q = 0; q < wid; ++q) base += L.s_wcnt[q];
+      int tot = 0;
+      for (int q = 0; q < TH / kWave; ++q) tot += L.s_wcnt[q];
+      const int e = base + __popcll(bm & ((1ull << lane) - 1ull));
       int hi = kHkHeavy;
-      if (cn > kHkWaveCn) {   // a heavy destination: a wave-parallel entry (order of entries immaterial)
-        const int e = atomicAdd(L.s_nheavy, 1);
-        if (e < kHkHeavy) {
-          hi = e;
-          L.s_heavy[e][0] = k;
-          L.s_heavy[e][1] = s;
-          L.s_heavy[e][2] = tid;
-          L.s_heavy[e][3] = cf | (cn << 8);
-        }
+      if (heavy && e < kHkHeavy) {
+        hi = e;
+        L.s_heavy[e][0] = k;
+        L.s_heavy[e][1] = s;
+        L.s_heavy[e][2] = tid;
+        L.s_heavy[e][3] = cf | (cn << 8);
       }
+      __syncthreads();   // every wave read s_nheavy and s_wcnt before they change
+      if (tid == 0) *L.s_nheavy = base + tot;   // (thread 0: wave 0, base = the running total)
       s_cinfo[(k * SMAX + s) * TH + tid] = hk_cinfo(cf, cn, hi);
     }
   }
@@ -1155,10 +1171,10 @@ __device__ __forceinline__ int hk_solve_inlined(HkArgs a, unsigned* nb_io, unsig
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok, s_wcnt[TH / kWave];
   __shared__ double s_hval[kHkHeavy];
   HkShared<SMAX, KC, TH> L{hk_dyn_in, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_wcnt, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
   const int mv = hk_solve<SMAX, KC, TH, PULL, FUSEA>(a, L, nb, ne);
   *nb_io = nb;
@@ -1179,10 +1195,10 @@ __device__ __noinline__ int hk_solve_isolated(HkArgs a, unsigned* nb_io, unsigne
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok, s_wcnt[TH / kWave];
   __shared__ double s_hval[kHkHeavy];
   HkShared<SMAX, KC, TH> L{hk_dyn, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_wcnt, s_heavy, s_hval, &s_rok};
   unsigned nb = *nb_io, ne = *ne_io;
   const int mv = hk_solve<SMAX, KC, TH, PULL, FUSEA>(a, L, nb, ne);
   *nb_io = nb;

@@ -54,10 +54,10 @@ __global__ __launch_bounds__(TH) void hist_bicg_kernel(HcRun r) {
   __shared__ double s_res[kHkRed];
   __shared__ int s_flag, s_stop;
   __shared__ int s_ex[2 * SMAX];
-  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok;
+  __shared__ int s_nheavy, s_heavy[kHkHeavy][4], s_rok, s_wcnt[TH / kWave];
   __shared__ double s_hval[kHkHeavy];
   HkShared<SMAX, KC, TH> L{Tacc, s_base, s_pub, &s_tot, s_cand, s_ncand, s_cinfo, s_P, s_part, s_res,
-                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_heavy, s_hval, &s_rok};
+                                 &s_flag, &s_stop, s_ex, &s_nheavy, s_wcnt, s_heavy, s_hval, &s_rok};
   const int G = r.G, S = r.S, n_a = r.n_a;
   const int lc = blockIdx.x / G;
   const int w = blockIdx.x - lc * G;

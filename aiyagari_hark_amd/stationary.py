@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import math
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -77,9 +78,24 @@ def _resolve_device(device):
 
 
 def firm_prices(r, alpha, delta):
-    """(w, K_demand) with L = 1 (Cobb-Douglas firm of calc_R_and_W, AS:1886-1890)."""
-    KtoL = (alpha / (r + delta)) ** (1.0 / (1.0 - alpha))
-    return (1.0 - alpha) * KtoL ** alpha, KtoL
+    """(w, K_demand) with L = 1 (Cobb-Douglas firm of calc_R_and_W, AS:1886-1890).
+
+    Element by element through libm's pow (math.pow), the function the native loops call
+    (csrc/ge.hip: std::pow): numpy's vectorised power is not correctly rounded on every CPU
+    (its AVX-512 form differs from libm in the last bit for ~10 % of rates), and a one-ulp
+    difference in w or K_d makes the Python and native GE loops take different steps."""
+    r, alpha, delta = np.broadcast_arrays(np.asarray(r, dtype=np.float64), np.asarray(alpha, dtype=np.float64),
+                                          np.asarray(delta, dtype=np.float64))
+    KtoL = np.empty(r.shape)
+    w = np.empty(r.shape)
+    for i in np.ndindex(r.shape):
+        a = float(alpha[i])
+        k = math.pow(a / (float(r[i]) + float(delta[i])), 1.0 / (1.0 - a))
+        KtoL[i] = k
+        w[i] = (1.0 - a) * math.pow(k, a)
+    if KtoL.ndim == 0:
+        return float(w), float(KtoL)
+    return w, KtoL
 
 
 @dataclass

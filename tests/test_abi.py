@@ -116,3 +116,23 @@ def test_option_constants_match_header():
     assert "AIY_OPT_GE_REBALANCE" in opts and "AIY_OPT_GE_EXTRAP_PERIOD" in opts
     for k, v in opts.items():
         assert getattr(_lib, k) == v, k
+
+
+def test_firm_prices_use_libm_pow():
+    """The Python GE loops price r through libm's pow, the function csrc/ge.hip calls
+    (std::pow): numpy's vectorised power differs from it in the last bit on AVX-512 hosts,
+    and one ulp of w moves a BiCGSTAB path."""
+    import math
+
+    import numpy as np
+
+    from aiyagari_hark_amd.stationary import firm_prices
+    rng = np.random.default_rng(5)
+    r = np.concatenate([[float.fromhex("0x1.2a359f8a72972p-5")], rng.uniform(-0.04, 0.04, 500)])
+    alpha = np.full_like(r, 0.36)
+    w, kd = firm_prices(r, alpha, 0.08)
+    for i in range(len(r)):
+        k = math.pow(0.36 / (r[i] + 0.08), 1.0 / (1.0 - 0.36))
+        assert kd[i] == k and w[i] == (1.0 - 0.36) * math.pow(k, 0.36)
+    ws, ks = firm_prices(0.03, 0.36, 0.08)
+    assert isinstance(ws, float) and ks == math.pow(0.36 / 0.11, 1.0 / 0.64)

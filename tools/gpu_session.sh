@@ -75,6 +75,8 @@ for step in "$@"; do
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
     suite) run suite 1000 $PYT -m gpu tests ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
+    determ) run determ 300 python -u tools/hist_determinism.py ge ;;
+    benchlegs) run benchlegs 600 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --legs table2,configs1,configs3,configs4 ;;
     bench_t2) run bench_t2 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     trace) export TMPDIR=/tmp; run trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --legs table2 ;;
     trace_c1) export TMPDIR=/tmp; run trace_c1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs1 ;;
@@ -86,6 +88,7 @@ for step in "$@"; do
     sharded) run sharded 500 $PYT -s tests/test_gpu_sharded.py tests/test_gpu_benchsize.py -k "configs3 or sharded or shard or rccl" ;;
     c3pred) run c3pred 400 python -u tools/c3_shard_predict.py ;;
     abc4) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abc4_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs configs4 --steps 1 --warmup 0 --no-cpu-baseline; done ;;
+    ablegs) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ablegs_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs ${LEGS:-configs1} --steps 2 --warmup 1 --no-cpu-baseline; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
