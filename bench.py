@@ -759,6 +759,8 @@ def main():
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     ap.add_argument("--ge-rebalance", type=int, default=None,
                     help="AIY_OPT_GE_REBALANCE for the resident searches (default: the library's)")
+    ap.add_argument("--hist-cluster", type=int, default=None,
+                    help="AIY_OPT_HIST_CLUSTER: workgroups per calibration cluster cap (default the library's)")
     ap.add_argument("--ge-loose-hist", type=int, default=None,
                     help="AIY_OPT_GE_LOOSE_HIST (loose-bracketing histogram tolerance 10^-v; default the library's)")
     args = ap.parse_args()
@@ -777,7 +779,8 @@ def main():
         build.build(verbose=False)
     barrier(world)
     legs = set(args.legs.split(","))
-    if args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None:
+    if (args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None or
+            args.hist_cluster is not None):
         from aiyagari_hark_amd import _lib
         opts = {}
         if args.hist_pull is not None:
@@ -786,6 +789,8 @@ def main():
             opts[_lib.AIY_OPT_GE_REBALANCE] = args.ge_rebalance
         if args.ge_loose_hist is not None:
             opts[_lib.AIY_OPT_GE_LOOSE_HIST] = args.ge_loose_hist
+        if args.hist_cluster is not None:
+            opts[_lib.AIY_OPT_HIST_CLUSTER] = args.hist_cluster
         _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]

@@ -143,7 +143,28 @@ def counts_mode():
                                   its=[np.asarray(c).tolist() for c in res.hist_iters])), flush=True)
 
 
+def sweep_mode(rebalance):
+    """The 24-cell Table II sweep (device-resident search) three times: r bit for bit.  With
+    rebalance = 0 the launch sequence does not depend on timing, so any difference comes from
+    the kernels."""
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd.stationary import solve_table2, table2_calibrations
+    dev = torch.device("cuda:0")
+    h = _lib.handle(0)
+    h.set_options({_lib.AIY_OPT_GE_REBALANCE: rebalance})
+    runs = []
+    for _ in range(3):
+        res = solve_table2(table2_calibrations(), n_a=10000, r_tol=1e-7, device=dev, method="brent", accel=-1)
+        runs.append([float(x).hex() for x in res.r])
+    same = all(r == runs[0] for r in runs)
+    ndiff = [sum(a != b for a, b in zip(runs[0], r)) for r in runs[1:]]
+    print(json.dumps(dict(lib=os.environ.get("AIYAGARI_LIB", "in-tree"), rebalance=rebalance, identical=same,
+                          cells_differing=ndiff, r0=runs[0][:4])))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "sweep":
+        return sweep_mode(int(sys.argv[2]) if len(sys.argv) > 2 else 0)
     if len(sys.argv) > 1 and sys.argv[1] == "counts":
         return counts_mode()
     if len(sys.argv) > 1 and sys.argv[1] == "warm":
