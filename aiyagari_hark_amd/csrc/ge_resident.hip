@@ -947,7 +947,7 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_m
 
 // The whole search on device when the shape allows it (1: done; 0: not applicable, the caller
 // runs the host-driven loop; < 0: error).  With rebalancing (AIY_OPT_GE_REBALANCE = q > 0,
-// default 50) a launch whose calibrations are more than 4 stops every cluster at its next
+// default 55) a launch whose calibrations are more than 4 stops every cluster at its next
 // evaluation boundary once q % of them have finished, and the unfinished ones are launched
 // again with the freed compute units (a cluster's time scales with its columns per CU): with
 // q = 50 the 24 Table II cells run as 24 x 10, then ~12 x 21, ~6 x 32, ~3 x 32 workgroups.

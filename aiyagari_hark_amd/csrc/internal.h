@@ -61,7 +61,7 @@ struct aiy_handle {
   // device-resident GE search (ge_resident.hip)
   bool ge_resident = false;          // AIY_OPT_GE_RESIDENT
   int cu_limit = 0;                  // AIY_OPT_CU_LIMIT: compute units resident launches may fill (0: all)
-  int ge_rebalance = 50;             // AIY_OPT_GE_REBALANCE: % finished that stops a launch (0: one launch)
+  int ge_rebalance = 55;             // AIY_OPT_GE_REBALANCE: % finished that stops a launch (0: one launch)
   int ge_rounds = 0;                 // launches of the last device-resident search
   int ge_mid_stops = 0;              // of its clusters, those stopped inside a distribution solve
   int ge_extrap_period = 32;         // AIY_OPT_GE_EXTRAP_PERIOD: EGM cycles between extrapolation checks

@@ -355,7 +355,7 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     (stationary.solve_table2) sets it by default */
 #define AIY_OPT_CU_LIMIT 11       /* compute units the resident launches of this handle may fill
                                     (0: the device's; several processes sharing one GPU: a share) */
-#define AIY_OPT_GE_REBALANCE 12   /* value q in [1, 100] (default 50): the device-resident GE search
+#define AIY_OPT_GE_REBALANCE 12   /* value q in [1, 100] (default 55): the device-resident GE search
                                     stops every cluster at an evaluation boundary once q % of a
                                     launch's calibrations have finished and relaunches the rest on
                                     the freed compute units (larger clusters); 0: one launch */

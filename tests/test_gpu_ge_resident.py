@@ -93,6 +93,7 @@ def test_rebalancing_relaunches_match_one_launch(gpu):
     h = _lib.handle(gpu.index)
     cals = table2_calibrations()
     kw = dict(n_a=3000, device=gpu, method="brent", resident=True)
+    prior = h.get_option(_lib.AIY_OPT_GE_REBALANCE)
     try:
         h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, 0), "opt")
         one = solve_table2(cals, **kw)
@@ -101,7 +102,7 @@ def test_rebalancing_relaunches_match_one_launch(gpu):
         launches, mid = ctypes.c_int32(), ctypes.c_int32()
         h.check(h.lib.aiy_ge_last_rounds(h.h, ctypes.byref(launches), ctypes.byref(mid)), "rounds")
     finally:
-        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, 50), "opt")
+        h.check(h.lib.aiy_set_option(h.h, _lib.AIY_OPT_GE_REBALANCE, prior), "opt")
     print(f"\nsteps one {one.bisection_steps} rebalanced {reb.bisection_steps}; max |dr| {np.max(np.abs(reb.r - one.r)):.2e}; "
           f"{launches.value} launches, {mid.value} stops inside a distribution solve")
     # relaunches happened, and some clusters stopped inside a BiCGSTAB solve (resumed from x)
