@@ -90,6 +90,7 @@ for step in "$@"; do
     abc4) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run abc4_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs configs4 --steps 1 --warmup 0 --no-cpu-baseline; done ;;
     dkc1) run dkc1_noisy 60 python -u tools/hist_determinism.py noisy 300 && run dkc1_nofusea 90 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_nofusea.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 3 --rebalance 0 && run dkc1_fusea 90 python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 3 --rebalance 0 ;;
     dpush) run dp_sweep 400 python -u tools/hist_determinism.py sweep 0 && run dp_sweep_head 400 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_headpush.so python -u tools/hist_determinism.py sweep 0 ;;
+    absub8) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run absub8_$v 300 env AIYAGARI_LIB=$lib python -u tools/table2_rank_subsets.py 8 32; done ;;
     ablegs) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ablegs_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs ${LEGS:-configs1} --steps 2 --warmup 1 --no-cpu-baseline; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
