@@ -43,6 +43,7 @@ AIY_OPT_GE_LOGSEC = 14
 AIY_OPT_HIST_PULL = 15
 AIY_OPT_GE_LOOSE_HIST = 17
 AIY_OPT_RESIDENT_SHAPE_STREAM = 18
+AIY_OPT_GE_ANDERSON = 23
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

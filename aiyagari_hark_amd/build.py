@@ -56,7 +56,8 @@ def needs_rebuild() -> bool:
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in sources() + HEADERS]
     deps.append(os.path.join(HERE, "..", "include", "aiyagari.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return (any(os.path.getmtime(d) > t for d in deps if os.path.exists(d)) or
+            library_digest(LIB) != source_digest())
 
 
 def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
@@ -68,14 +69,27 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     cc = hipcc()
     flags = [f"--offload-arch={ARCH}"] + CFLAGS + [f"-D{d}" for d in defines]
 
+    # objects are kept next to the library and rebuilt only when their source, a header or the
+    # flags changed (a header change rebuilds everything)
+    stamp = os.path.join(objdir, "flags.txt")
+    same_flags = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
+    hdr_t = max([os.path.getmtime(os.path.join(CSRC, f)) for f in HEADERS if os.path.exists(os.path.join(CSRC, f))] +
+                [os.path.getmtime(os.path.join(HERE, "..", "include", "aiyagari.h"))])
+
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [cc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if (same_flags and not force and os.path.exists(obj) and
+                os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src)))):
+            return obj
+        cmd = [cc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj + ".tmp.o"]
         if verbose:
             print("[aiyagari build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp.o", obj)
         return obj
 
+    if not same_flags:
+        open(stamp, "w").write(" ".join(flags))
     jobs = min(len(sources()), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, sources()))
@@ -83,10 +97,24 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-L/opt/rocm/lib", "-lrccl", "-o", tmp]
     if verbose:
         print("[aiyagari build]", " ".join(cmd), flush=True)
+    # computed before linking: the sources this library was built from (+ any diagnostic defines,
+    # so a variant build never passes for the product library)
+    digest = source_digest() + ("+" + ",".join(defines) if defines else "")
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
-    shutil.rmtree(objdir, ignore_errors=True)
+    # sidecar: the source digest the library was built from (tools/prof_bench.sh stamps a PMC
+    # pass with the digest of the library the bench actually loads, not just of the sources)
+    with open(out + ".digest", "w") as f:
+        f.write(digest + "\n")
     return out
+
+
+def library_digest(path: str = LIB):
+    """The source digest a built library was made from (its .digest sidecar), or None."""
+    try:
+        return open(path + ".digest").read().strip() or None
+    except OSError:
+        return None
 
 
 def build_variant(name: str, defines) -> str:

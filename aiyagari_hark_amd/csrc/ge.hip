@@ -152,7 +152,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     const double hi0 = o->r_hi ? o->r_hi[c] : 1.0 / M->disc[c] - 1.0 - 1e-9;
     rs[c].init(lo0, hi0, o->r_tol, o->method, o->loose_bracket != 0 ? h->ge_logsec : 0);
   }
-  std::vector<double> R(n_cal), w(n_cal), Kd(n_cal), Ks(n_cal, 0.0);
+  std::vector<double> R(n_cal), w(n_cal), Kd(n_cal), Ks(n_cal, 0.0), Ks_fin(n_cal, 0.0);
   std::vector<int32_t> cyc(n_cal), its(n_cal);
   std::vector<double> dist(n_cal);
   aiy_egm_dims dims{n_cal, S, 1, n_a};
@@ -161,12 +161,22 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
   int steps = 0;
   int32_t rc = AIY_OK;
   long long cyc_sum = 0, it_sum = 0;
-  while (steps < o->max_steps) {
+  // a calibration whose search ends on an evaluation at looser tolerances (loose
+  // bracketing, or Brent's adaptive distribution tolerance) has that r evaluated once more at
+  // egm_tol / hist_tol (warm: a few cycles and matvecs) before its K_s is reported; fin[c] marks
+  // it for that final pass, which evaluates r_cur[c] (the others re-evaluate their rs.x as every
+  // step does for finished calibrations)
+  std::vector<char> fin(n_cal, 0);
+  bool final_pass = false;
+  while (steps < o->max_steps || final_pass) {
     bool all_done = true;
     for (int c = 0; c < n_cal; ++c) all_done = all_done && rs[c].done;
-    if (all_done) break;
+    if (all_done && !final_pass) {
+      for (int c = 0; c < n_cal; ++c) final_pass = final_pass || fin[c];
+      if (!final_pass) break;
+    }
     for (int c = 0; c < n_cal; ++c) {
-      const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];
+      const double r = fin[c] ? r_cur[c] : rs[c].x, a = M->alpha[c], d = M->delta[c];
       const double KtoL = std::pow(a / (r + d), 1.0 / (1.0 - a));
       R[c] = 1.0 + r;
       w[c] = (1.0 - a) * std::pow(KtoL, a);
@@ -203,7 +213,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     if (secant) {
       for (int c = 0; c < n_cal; ++c) {
         const double den = r_cur[c] - r_prev[c];
-        double th = den != 0.0 ? (rs[c].x - r_cur[c]) / den : 0.0;
+        double th = den != 0.0 && !fin[c] ? (rs[c].x - r_cur[c]) / den : 0.0;
         theta[c] = std::isfinite(th) ? std::max(-1.0, std::min(1.0, th)) : 0.0;
       }
       AIY_HIP(h, hipMemcpyAsync(d_th, theta.data(), sizeof(double) * n_cal, hipMemcpyHostToDevice, st));
@@ -254,7 +264,19 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     h->hist_krylov = saved_krylov;
     h->egm_tolv = h->egm_tolh = h->hist_tolv = nullptr;
     if (rc) break;
+    if (final_pass) {   // K_s of the marked calibrations at the full tolerances; the search is over
+      for (int c = 0; c < n_cal; ++c)
+        if (fin[c]) {
+          cyc_sum += cyc[c];
+          it_sum += its[c];
+          if (cyc[c] > max_cyc && !(dist[c] <= etol[c])) status[c] |= 1;
+          if (its[c] >= max_hist) status[c] |= 2;
+          Ks_fin[c] = Ks[c];
+        }
+      break;
+    }
     for (int c = 0; c < n_cal; ++c) {
+      const bool was_done = rs[c].done;
       cyc_sum += cyc[c];
       it_sum += its[c];
       // an evaluation that stopped at an iteration cap still moves the bracket by its sign;
@@ -270,6 +292,8 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
         rs[c].update(f, Kd[c]);
         fmin_rel[c] = std::min(fmin_rel[c], std::fabs(f) / Kd[c]);
       }
+      if (!was_done && rs[c].done) fin[c] = loose[c] || adapt[c];
+      Ks_fin[c] = Ks[c];
     }
     ++steps;
   }
@@ -281,7 +305,7 @@ extern "C" int32_t aiy_ge_stationary(aiy_handle* h, const aiy_stationary_model* 
     const double r = rs[c].x, a = M->alpha[c], d = M->delta[c];
     r_out[c] = r;
     K_out[c] = std::pow(a / (r + d), 1.0 / (1.0 - a));
-    if (Ks_out) Ks_out[c] = Ks[c];
+    if (Ks_out) Ks_out[c] = Ks_fin[c];
   }
   for (int c = 0; c < n_cal; ++c)
     if (!rs[c].done) status[c] |= 4;

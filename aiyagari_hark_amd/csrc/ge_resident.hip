@@ -52,6 +52,15 @@ constexpr int kGeTHMax = 1024;
 constexpr int kGeWavesMax = kGeTHMax / kWave;   // 16
 constexpr int kGeMaxTiles = 16;           // 64-node tiles of one workgroup's own columns (<= 1024)
 constexpr int kGeBufs = 5;                // table buffers per calibration: ping, pong, cur, prev, init
+// Periodic Anderson mixing of the EGM cycles (AIY_OPT_GE_ANDERSON): every p-th cycle the
+// household iterate moves to the type-II Anderson combination of the last kGeAaM + 1 plain
+// cycles (their outputs kept in a ring of kGeAaHist slots), plain cycles in between.  A CPU
+// study on the oracle's EGM (scratch prototype; N_a = 3 000, the Table II cells near their
+// roots, warm and cold starts) put it at 1.5-2.5x fewer cycles to the same HARK stopping rule
+// than the period-32 geometric extrapolation it replaces (m = 3, p = 12: 97-128 against
+// 196-248 cycles from a start 2e-2 away in r, 49-97 against 112-178 from 2e-5).
+constexpr int kGeAaM = 3;
+constexpr int kGeAaHist = kGeAaM + 2;
 // One asset column per thread (G >= 20 at N_a = 10 000: every relaunch and the 8-GPU shape):
 // the BiCGSTAB solve's alpha reduction rides on its first matvec's barrier (hist_bicg.h
 // FUSEA), one cluster reduction per iteration instead of two.  A diagnostic build with
@@ -61,6 +70,16 @@ constexpr bool kGeFuseA = false;
 #else
 constexpr bool kGeFuseA = true;
 #endif
+// With two columns per thread (the first, 24-cell launch of a Table II sweep) the default keeps the
+// two-reduction form: FUSEA there (-DAIY_FUSEA_KC2=2: u's own points read back from HBM beside the
+// new p; =1: prefetched across the second reduction) measured SLOWER, 411-427 against 481-491 GE
+// solves/s for the Table II sweep (gpurun_out/r08e_abaa_*: the last wave, which sweeps the riding
+// reduction, owns columns at two per thread and delays its gather; the x loads move behind the
+// matvec)
+#ifndef AIY_FUSEA_KC2
+#define AIY_FUSEA_KC2 0
+#endif
+constexpr bool kGeFuseAKc2 = AIY_FUSEA_KC2 != 0;
 template <int NW>
 constexpr size_t ge_egm_lds() { return (size_t)NW * (8 * kTile + 4 * kWin) * sizeof(double); }   // V tiles + windows
 
@@ -82,6 +101,8 @@ struct GeRun {
   int max_steps, max_cyc, max_hist;
   int warm_hist, warm_egm, secant, loose, extrap;
   int extrap_period;      // EGM cycles between extrapolation checks (>= 4)
+  int aa_period;          // EGM Anderson mixing every aa_period cycles (0: off; AIY_OPT_GE_ANDERSON)
+  double* aah;            // [n_cal][kGeAaHist][S][n_a] the last kGeAaHist EGM outputs (c, own nodes)
   int logsec;             // log-secant bracketing (AIY_OPT_GE_LOGSEC, with loose bracketing)
   int pull;               // distribution solves by the lottery pull (AIY_OPT_HIST_PULL): deterministic
   double loose_hist;      // loose-bracketing histogram tolerance (AIY_OPT_GE_LOOSE_HIST)
@@ -132,6 +153,8 @@ struct GeState {
   int adapt;               // this evaluation runs at an adaptive histogram tolerance
   int steps, loose, refine, warm_egm, secant, fresh_mass, status, n, stop, nan_stop, moved, extrap;
   int in_hist;             // stopped (rebalancing) inside this evaluation's distribution solve
+  int final_ks;            // the search ended on a loose or adaptive-tolerance evaluation: that r is
+                           // evaluated once more at the full tolerances before K_s is reported
   int buf[kGeBufs];        // roles: 0 ping, 1 pong, 2 cur, 3 prev, 4 init -> buffer index
   long long cyc_sum, its_sum;
   unsigned long long t_egm, t_lot, t_hist, t_k, t0, t_ev0;
@@ -298,7 +321,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
                                                const double* src_m, const double* src_c, double* dst_m,
                                                double* dst_c, bool track, double R, double beta, double gam,
                                                const double* s_Wl, const double* s_Pe, int* s_hint,
-                                               double* lds_v, double* lds_win) {
+                                               double* lds_v, double* lds_win, double* ring) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int n1 = n_a + 1;
@@ -322,6 +345,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
         const double c = inv_marg<PK>(beta * sum, gam);
         store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], a + c);
         store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
+        if (ring) store_f64_agent(&ring[(size_t)s * n_a + j], c);
         if (j == 0) {
           store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
           store_f64_agent(&dst_c[(size_t)s * n1], kBorrowNode);
@@ -359,6 +383,7 @@ __device__ __forceinline__ double ge_egm_cycle(int S, int n_a, int j0, int j1, c
         const double m = a + c;                          // AS:1499
         store_f64_agent(&dst_m[(size_t)s * n1 + j + 1], m);
         store_f64_agent(&dst_c[(size_t)s * n1 + j + 1], c);
+        if (ring) store_f64_agent(&ring[(size_t)s * n_a + j], c);   // Anderson history (own nodes)
         if (track) dmax = nan_max(dmax, nan_max(fabs(m - pmv[s]), fabs(c - pcv[s])));
         if (j == 0) {   // the (1e-7, 1e-7) node (AS:1503-1504)
           store_f64_agent(&dst_m[(size_t)s * n1], kBorrowNode);
@@ -391,9 +416,10 @@ __shared__ GeState ge_st;
 template <int SMAX, int SC, int PK, int NW>
 __device__ __forceinline__ double ge_egm_cycle_fn(int S, int n_a, int j0, int j1, const double* a_grid,
                                                const double* src_m, const double* src_c, double* dst_m,
-                                               double* dst_c, bool track, double R, double beta, double gam) {
+                                               double* dst_c, bool track, double R, double beta, double gam,
+                                               double* ring) {
   return ge_egm_cycle<SMAX, SC, PK, NW>(S, n_a, j0, j1, a_grid, src_m, src_c, dst_m, dst_c, track, R, beta, gam,
-                                        ge_s_Wl, ge_s_Pe, ge_s_hint, ge_dyn, ge_dyn + (size_t)NW * SMAX * kTile);
+                                        ge_s_Wl, ge_s_Pe, ge_s_hint, ge_dyn, ge_dyn + (size_t)NW * SMAX * kTile, ring);
 }
 
 // lottery of the own columns on the final tables (hist.hip hist_lottery_kernel's arithmetic)
@@ -488,6 +514,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       st.steps = 0;
       st.refine = 0;
       st.in_hist = 0;
+      st.final_ks = 0;
       st.status = 0;
       st.cyc_sum = st.its_sum = 0;
       for (int b = 0; b < kGeBufs; ++b) st.buf[b] = b;
@@ -505,7 +532,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
   };
 
   bool stopped = false;
-  while (!st.rs.done && st.steps < g.max_steps) {
+  while ((!st.rs.done && st.steps < g.max_steps) || st.final_ks) {
     // ---- rebalancing stop: once stop_at calibrations of the launch have finished, the
     //      cluster leaves at this evaluation boundary (the decision: any workgroup saw it,
     //      counted on the cluster's barrier, so every workgroup takes it) ----
@@ -538,7 +565,8 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
     if (!st.in_hist) {
       // ---- this evaluation's prices, tolerances and starts (thread 0; identical everywhere) ----
       if (tid == 0) {
-        const double r = st.rs.x, a = cd.alpha, d = cd.delta;
+        // (the final pass re-evaluates the LAST evaluated r at the full tolerances)
+        const double r = st.final_ks ? st.r_cur : st.rs.x, a = cd.alpha, d = cd.delta;
         const double KtoL = pow(a / (r + d), 1.0 / (1.0 - a));
         st.R = 1.0 + r;
         st.wage = (1.0 - a) * pow(KtoL, a);
@@ -553,7 +581,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
           st.adapt = st.htol > g.hist_tol;
         }
         st.warm_egm = g.warm_egm && st.steps > 0;
-        st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2;
+        st.secant = g.secant && g.warm_egm && g.warm_hist && st.steps >= 2 && !st.final_ks;
         st.fresh_mass = !(g.warm_hist && st.steps > 0);
         double th = 0.0;
         if (st.secant) {
@@ -594,7 +622,13 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       int final_buf = -1;
       for (int attempt = 0; attempt < 2; ++attempt) {
         if (!plain_barrier()) return;   // every workgroup's start tables visible
-        const bool ext = st.extrap != 0 && attempt == 0;
+        // Anderson mixing (the first attempt; a NaN after a mix reruns the solve plain) replaces
+        // the geometric extrapolation
+        const bool aa = g.aa_period > 0 && attempt == 0;
+        const bool ext = st.extrap != 0 && attempt == 0 && !aa;
+        auto ring_at = [&](int c) -> double* {
+          return aa ? g.aah + ((size_t)cal * kGeAaHist + (size_t)(c % kGeAaHist)) * S * n_a : nullptr;
+        };
         if (tid == 0) {
           st.lam_prev = -1.0;
           st.moved = 0;
@@ -611,16 +645,16 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
           double dl;
           if (pk == 1)
             dl = ge_egm_cycle_fn<SMAX, SC, 1, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                              gam);
+                                              gam, ring_at(n));
           else if (pk == 3)
             dl = ge_egm_cycle_fn<SMAX, SC, 3, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                              gam);
+                                              gam, ring_at(n));
           else if (pk == 5)
             dl = ge_egm_cycle_fn<SMAX, SC, 5, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                              gam);
+                                              gam, ring_at(n));
           else
             dl = ge_egm_cycle_fn<SMAX, SC, 0, NW>(S, n_a, j0, j1, a_grid, sm, sc, tabm(b_dst), tabc(b_dst), track, R, beta,
-                                              gam);
+                                              gam, ring_at(n));
           // cluster distance: the value itself at the extrapolation checks (cycles 32k - 1,
           // 32k), else only its two facts (some part > tol; some part NaN) on a counting barrier
           const int xp = g.extrap_period;
@@ -692,6 +726,62 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
             }
           } else if (want_value) {
             if (tid == 0) st.dist = dclu;
+          }
+          if (aa && n >= g.aa_period && n >= kGeAaHist + 1 && (n % g.aa_period) == 0) {
+            // type-II Anderson over the plain chain w0 .. w4 = the outputs of cycles n - 4 .. n
+            // (p >= kGeAaHist: no mix inside the window): g_i = w_{i+1} - w_i, dG_i = g_{i+1} - g_i,
+            // dF_i = w_{i+2} - w_{i+1}; gamma = argmin |g_3 - dG gamma| (Gram + 1e-12 trace
+            // regularisation, two cluster reductions in fixed order: every workgroup solves the
+            // same 3 x 3 system to the same bits); x_{n+1} = w4 - dF gamma replaces the cycle's
+            // output (own nodes, m = a + c), visible to every workgroup after a barrier
+            static_assert(kGeAaM == 3 && kGeAaHist == 5, "the mixing below is written for m = 3");
+            const double* W0 = ring_at(n - 4);
+            const double* W1 = ring_at(n - 3);
+            const double* W2 = ring_at(n - 2);
+            const double* W3 = ring_at(n - 1);
+            const double* W4 = ring_at(n);
+            double gp[9];
+            for (int q = 0; q < 9; ++q) gp[q] = 0.0;
+            for (int s = 0; s < S; ++s)
+              for (int k = j0 + tid; k < j1; k += TH) {
+                const size_t o = (size_t)s * n_a + k;
+                const double w0 = load_f64_agent(W0 + o), w1 = load_f64_agent(W1 + o), w2 = load_f64_agent(W2 + o);
+                const double w3 = load_f64_agent(W3 + o), w4 = load_f64_agent(W4 + o);
+                const double g0 = w1 - w0, g1 = w2 - w1, g2 = w3 - w2, g3 = w4 - w3;
+                const double d0 = g1 - g0, d1 = g2 - g1, d2 = g3 - g2;
+                gp[0] += d0 * d0; gp[1] += d0 * d1; gp[2] += d0 * d2;
+                gp[3] += d1 * d1; gp[4] += d1 * d2; gp[5] += d2 * d2;
+                gp[6] += d0 * g3; gp[7] += d1 * g3; gp[8] += d2 * g3;
+              }
+            if (!ge_reduce<TH>(gran, G, w, ne, gp, 6, 0u, s_part, s_res, &s_flag, g.err)) return;
+            double a00 = s_res[0], a01 = s_res[1], a02 = s_res[2], a11 = s_res[3], a12 = s_res[4], a22 = s_res[5];
+            if (!ge_reduce<TH>(gran, G, w, ne, gp + 6, 3, 0u, s_part, s_res, &s_flag, g.err)) return;
+            const double b0 = s_res[0], b1 = s_res[1], b2 = s_res[2];
+            // Cholesky of the regularised Gram matrix (symmetric positive definite)
+            const double reg = 1e-12 * (a00 + a11 + a22);
+            a00 += reg; a11 += reg; a22 += reg;
+            const double l00 = sqrt(a00), l10 = a01 / l00, l20 = a02 / l00;
+            const double l11 = sqrt(a11 - l10 * l10), l21 = (a12 - l20 * l10) / l11;
+            const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
+            const double y0 = b0 / l00, y1 = (b1 - l10 * y0) / l11, y2 = (b2 - l20 * y0 - l21 * y1) / l22;
+            const double c2 = y2 / l22, c1 = (y1 - l21 * c2) / l11, c0 = (y0 - l10 * c1 - l20 * c2) / l00;
+            // (a degenerate or non-finite system -- a converging chain whose differences vanish,
+            // NaN nodes -- skips the mix: the cycle's output stands)
+            if (isfinite(c0) && isfinite(c1) && isfinite(c2) && reg > 0.0) {
+              double* dm = tabm(b_dst);
+              double* dc = tabc(b_dst);
+              for (int s = 0; s < S; ++s)
+                for (int k = j0 + tid; k < j1; k += TH) {
+                  const size_t o = (size_t)s * n_a + k;
+                  const double w1 = load_f64_agent(W1 + o), w2 = load_f64_agent(W2 + o);
+                  const double w3 = load_f64_agent(W3 + o), w4 = load_f64_agent(W4 + o);
+                  const double cn = w4 - ((c0 * (w2 - w1) + c1 * (w3 - w2)) + c2 * (w4 - w3));
+                  store_f64_agent(&dm[(size_t)s * n1 + k + 1], a_grid[k] + cn);   // AS:1499
+                  store_f64_agent(&dc[(size_t)s * n1 + k + 1], cn);
+                }
+              if (tid == 0) st.moved = 1;
+              if (!plain_barrier()) return;
+            }
           }
           ++n;
         }
@@ -766,7 +856,7 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       hk.Ainv = to_global(g.ainv + (size_t)cal * S * (n_a + 1));
       hk.lottery_fresh = true;
       mv = g.pull ? hk_solve_inlined<SMAX, KC, TH, true>(hk, &nb, &ne)
-                  : hk_solve_isolated<SMAX, KC, TH, false, KC == 1 && kGeFuseA>(hk, &nb, &ne);
+                  : hk_solve_isolated<SMAX, KC, TH, false, (KC == 1 || kGeFuseAKc2) && kGeFuseA>(hk, &nb, &ne);
     }
     if (mv == -1) return;
     if (tid == 0) {
@@ -796,9 +886,10 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       double v[1] = {part};
       if (!ge_reduce<TH>(gran, G, w, ne, v, 1, 0u, s_part, s_res, &s_flag, g.err)) return;
     }
+    const bool fin = st.final_ks != 0;   // (set in an earlier pass; never cleared: the loop ends here)
     if (tid == 0) {
       const double Ks = s_res[0];
-      if (w == 0 && st.steps < kGeEvLog) {
+      if (w == 0 && st.steps < kGeEvLog && !fin) {
         double* ev = g.out_evlog + ((size_t)cal * kGeEvLog + st.steps) * kGeEvRec;
         ev[0] = st.rs.x;
         ev[1] = (Ks - st.Kd) / st.Kd;
@@ -809,6 +900,14 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       }
       st.its_sum += mv;
       if (mv >= g.max_hist) st.status |= 2;
+    }
+    if (fin) {   // the full-tolerance re-solve of the last evaluation: K_s only
+      if (tid == 0) st.Ks = s_res[0];
+      __syncthreads();
+      break;
+    }
+    if (tid == 0) {
+      const double Ks = s_res[0];
       st.r_prev = st.r_cur;
       st.r_cur = st.rs.x;
       const double f = Ks - st.Kd;
@@ -820,6 +919,11 @@ __global__ __launch_bounds__(TH) void ge_cluster_kernel(GeRun g) {
       }
       st.Ks = Ks;
       ++st.steps;
+      // a search that ends on an evaluation at looser tolerances (a loose bracketing
+      // one, or Brent's at the adaptive distribution tolerance) reports K_s only after that r is
+      // evaluated again at egm_tol / hist_tol (one more pass, warm from its tables and mass: a few
+      // cycles and matvecs; searches normally end on full-tolerance evaluations near the root)
+      if (st.rs.done && (st.adapt || st.loose)) st.final_ks = 1;
       st.t_k += __builtin_amdgcn_s_memrealtime() - tp;
     }
     __syncthreads();
@@ -913,7 +1017,7 @@ static bool ge_make_plan(aiy_handle* h, int n_cal, int S, int n_a, GePlan& p) {
 
 struct GeScratch {
   size_t tab, mass, pmass, pg, qb, ainv, lo, wlo, slab, span, ctr, gran, ids, saved, resume, done, err, cal, outd, outi, prof,
-      evlog, bytes;
+      evlog, aah, bytes;
 };
 // Per-calibration arrays (kept across the rebalancing launches) first, then the per-launch
 // cluster arrays sized for the most workgroups any launch can hold (cus) and the largest span
@@ -941,6 +1045,7 @@ static GeScratch ge_scratch_layout(int n_cal, int S, int n_a, int cus, int cap_m
   L.outi = take((size_t)n_cal * 4 * sizeof(int));
   L.prof = take((size_t)n_cal * kGeProf * sizeof(double));
   L.evlog = take((size_t)n_cal * kGeEvLog * kGeEvRec * sizeof(double));
+  L.aah = take((size_t)n_cal * kGeAaHist * S * n_a * sizeof(double));
   L.bytes = o;
   return L;
 }
@@ -990,6 +1095,8 @@ int32_t ge_stationary_resident(aiy_handle* h, const aiy_stationary_model* M, con
   g.warm_hist = o->warm_hist != 0; g.warm_egm = o->warm_egm != 0;
   g.secant = o->secant_start != 0; g.loose = o->loose_bracket != 0; g.extrap = o->egm_extrapolate != 0;
   g.extrap_period = h->ge_extrap_period;
+  g.aa_period = o->egm_extrapolate != 0 ? h->ge_anderson : 0;   // (with the EGM acceleration on)
+  g.aah = reinterpret_cast<double*>(base + L.aah);
   g.logsec = h->ge_logsec;
   g.tab = reinterpret_cast<double*>(base + L.tab);
   g.mass = reinterpret_cast<double*>(base + L.mass);

@@ -832,45 +832,6 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   };
   auto matvec_r = [&](const double (&q)[KC][SMAX], double (&out)[KC][SMAX], const double* vals, int nv,
                       unsigned kmax) -> bool { return matvec_rp([&] { push(q); }, out, vals, nv, kmax); };
-  // one column per thread: the lottery of the own column loaded ahead of the push (in flight
-  // across the vector updates before it), and the push from those registers
-  auto load_lot = [&](int (&dp)[SMAX], double (&wp)[SMAX]) {
-    const int jc = col();
-#pragma unroll
-    for (int s = 0; s < SMAX; ++s) {
-      const bool ok = s < S && jc < j1;
-      const int q = min(s, S - 1) * n_a + min(jc, n_a - 1);
-      const int dv = LO[q];
-      const double wv = WL[q];
-      dp[s] = ok ? dv : -1;
-      wp[s] = ok ? wv : 0.0;
-    }
-  };
-  auto push_pre = [&](const double (&q)[KC][SMAX], const int (&dp)[SMAX], const double (&wp)[SMAX]) {
-    const bool act = j0 + tid < j1;
-#pragma unroll
-    for (int s = 0; s < SMAX; ++s) {
-      if (s < S) {   // wave-uniform
-        const int d = dp[s];
-        const double vlo = wp[s] * q[0][s];          // np.add.at(T[s], lo, wlo q)
-        const double vhi = (1.0 - wp[s]) * q[0][s];  // np.add.at(T[s], lo + 1, (1 - wlo) q)
-        const int ilo = __builtin_amdgcn_readlane(v_base, s) + d, ihi = ilo + 1;
-        const int d0 = __builtin_amdgcn_readfirstlane(d);
-        if (__all(act && d == d0)) {   // the whole wave on one destination (borrowing constraint)
-          const double tl = wave_sum_lane63(vlo), th = wave_sum_lane63(vhi);
-          if (lane == kWave - 1) {
-            atomicAdd(&Tacc[ilo], tl);
-            if (th != 0.0) atomicAdd(&Tacc[ihi], th);
-          }
-        } else if (act) {
-          if (vlo != 0.0) atomicAdd(&Tacc[ilo], vlo);
-          if (vhi != 0.0) atomicAdd(&Tacc[ihi], vhi);
-        }
-      }
-    }
-    __syncthreads();
-  };
-
   // ---- BiCGSTAB ----
   // registers: r (then s), p, and the matvec result; v waits in LDS (behind the spans) and
   // p in the HBM scratch row across the second matvec, whose gather needs the registers
@@ -900,28 +861,43 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
   double* Ug = (double*)r.Qg;
   double pu = 0.0;   // this thread's part of <u, p>
   auto make_u = [&]() {   // u of the own points -> Ug; pu = <u, p> with p = r
-    static_assert(!FUSEA || kLoReg, "FUSEA: the lottery of the own column in registers");
     if constexpr (FUSEA) {
       const int jc = col();
       double acc = 0.0;
 #pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        if (own(jc, 0, s)) {
-          const int d = dreg[0][s];
-          const double wl = wreg[0][s];
-          double tr = 0.0;
-          for (int sp = 0; sp < S; ++sp) {
-            const unsigned q = (unsigned)(sp * n_a + d) + seed * 0x5BD1E995u;
-            tr += s_P[s * SMAX + sp] * (wl * hk_rhat(q) + (1.0 - wl) * hk_rhat(q + 1u));
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          if (own(jc, k, s)) {
+            int d;
+            double wl;
+            if constexpr (kLoReg) {
+              d = dreg[k][s];
+              wl = wreg[k][s];
+            } else {   // (two columns per thread: the own lottery from L2, once per solve)
+              d = LO[gidx(jc, k, s)];
+              wl = WL[gidx(jc, k, s)];
+            }
+            double tr = 0.0;
+            for (int sp = 0; sp < S; ++sp) {
+              const unsigned q = (unsigned)(sp * n_a + d) + seed * 0x5BD1E995u;
+              tr += s_P[s * SMAX + sp] * (wl * hk_rhat(q) + (1.0 - wl) * hk_rhat(q + 1u));
+            }
+            const double u = rh_at(jc, k, s) - tr;
+            Ug[gidx(jc, k, s)] = u;
+            acc += u * pv[k][s];
           }
-          const double u = rh_at(jc, 0, s) - tr;
-          Ug[gidx(jc, 0, s)] = u;
-          acc += u * pv[0][s];
         }
-      }
       pu = acc;
     }
   };
+  // FUSEA with two columns per thread: u of the own points is read back when the new p is formed
+  // (AIY_FUSEA_KC2 = 1: prefetched with x and p across the second reduction; 2: loaded after it,
+  // beside the new p, so it holds no registers across the reduction)
+#ifndef AIY_FUSEA_KC2
+#define AIY_FUSEA_KC2 0
+#endif
+  constexpr bool kUqPre = KC == 1 || AIY_FUSEA_KC2 == 1;
   HK_PH(-1);
   while (true) {
     if (restart) {
@@ -991,24 +967,31 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     int jc;
     if constexpr (FUSEA) {
       // <u, p> and max|r| ride on this matvec's barrier (the stop request as a sentinel on the
-      // max, which no residual of a mass vector reaches); x's loads in flight across it
+      // max, which no residual of a mass vector reaches); x's loads in flight across it (one
+      // column per thread; with two, x is loaded after the matvec: its registers are full)
       jc = col();
       double rm = 0.0;
 #pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        if (own(jc, 0, s)) rm = nan_max(rm, fabs(Vl[vidx(0, s)]));
-        xq[0][s] = X[min(s, S - 1) * n_a + min(jc, n_a - 1)];
-      }
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          if (own(jc, k, s)) rm = nan_max(rm, fabs(Vl[vidx(k, s)]));
+          if constexpr (KC == 1) xq[k][s] = X[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
+        }
       part[0] = pu;
       part[1] = (r.stop_ctr != nullptr && tid == 0 && s_stop) ? kHkStopSentinel : rm;
       if (!matvec_r(pv, tv, part, 2, 2u)) return -1;
       ++mv;
+      jc = col();
 #pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        const double v = pv[0][s] - tv[0][s];
-        rv[0][s] = Vl[vidx(0, s)];
-        Vl[vidx(0, s)] = v;
-      }
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) {
+          const double v = pv[k][s] - tv[k][s];
+          rv[k][s] = Vl[vidx(k, s)];
+          Vl[vidx(k, s)] = v;
+          if constexpr (KC > 1) xq[k][s] = X[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
+        }
     } else {
       if (!matvec(pv, tv)) return -1;
       ++mv;
@@ -1099,7 +1082,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
     part[3] = rt;
     part[4] = sm;
     double pq[KC][SMAX];   // x and p of the own points, for x += omega s and the new p
-    double uq[FUSEA ? KC : 1][SMAX];   // FUSEA: u of the own points, for <u, p> of the new p
+    double uq[FUSEA && kUqPre ? KC : 1][SMAX];   // FUSEA: u of the own points, for <u, p> of the new p
     if (!reduce(part, 5, 16u, [&] {
           const int jq = col();
 #pragma unroll
@@ -1109,7 +1092,7 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
               const int g = min(s, S - 1) * n_a + min(jq + k * TH, n_a - 1);
               xq[k][s] = X[g];
               pq[k][s] = Pg[g];
-              if constexpr (FUSEA) uq[k][s] = Ug[g];
+              if constexpr (FUSEA && kUqPre) uq[k][s] = Ug[g];
             }
         }))
       return -1;
@@ -1134,9 +1117,21 @@ __device__ __forceinline__ int hk_solve(const HkArgs& r, const HkShared<SMAX, KC
         const double pold = ow ? pq[k][s] : 0.0;
         rv[k][s] = rv[k][s] - omega * tv[k][s];
         pv[k][s] = rv[k][s] + beta * (pold - omega * Vl[vidx(k, s)]);
-        if constexpr (FUSEA)
+        if constexpr (FUSEA && kUqPre)
           if (ow) pun += uq[k][s] * pv[k][s];
       }
+    if constexpr (FUSEA && !kUqPre) {   // u read back beside the new p (every load before the first use)
+      double ul[KC][SMAX];
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) ul[k][s] = Ug[min(s, S - 1) * n_a + min(jc + k * TH, n_a - 1)];
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s)
+          if (own(jc, k, s)) pun += ul[k][s] * pv[k][s];
+    }
     pu = pun;
     if (!(fabs(beta) < 1e300) || rho == 0.0) restart = true;
   }

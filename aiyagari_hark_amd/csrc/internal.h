@@ -65,6 +65,7 @@ struct aiy_handle {
   int ge_rounds = 0;                 // launches of the last device-resident search
   int ge_mid_stops = 0;              // of its clusters, those stopped inside a distribution solve
   int ge_extrap_period = 32;         // AIY_OPT_GE_EXTRAP_PERIOD: EGM cycles between extrapolation checks
+  int ge_anderson = 12;              // AIY_OPT_GE_ANDERSON: EGM cycles between Anderson mixes (0: off)
   int ge_logsec = 2;                 // AIY_OPT_GE_LOGSEC: 0 off, 1 two-point log-secant bracketing, 2 also from one point (with loose bracketing)
   void* d_ge = nullptr;              // tables, masses, lottery, cluster sync of the launch
   size_t ge_cap = 0;

@@ -510,6 +510,11 @@ extern "C" int32_t aiy_set_option(aiy_handle* h, int32_t option, int64_t value) 
       if (value < 4 || value > 1024) return fail(h, AIY_ERR_ARG, "AIY_OPT_GE_EXTRAP_PERIOD must be in [4, 1024]");
       h->ge_extrap_period = (int)value;
       return AIY_OK;
+    case AIY_OPT_GE_ANDERSON:
+      if (value != 0 && (value < 5 || value > 1024))
+        return fail(h, AIY_ERR_ARG, "AIY_OPT_GE_ANDERSON must be 0 or in [5, 1024]");
+      h->ge_anderson = (int)value;
+      return AIY_OK;
     case AIY_OPT_GE_REBALANCE:
       if (value < 0 || value > 100) return fail(h, AIY_ERR_ARG, "AIY_OPT_GE_REBALANCE must be in [0, 100]");
       h->ge_rebalance = (int)value;
@@ -545,6 +550,7 @@ extern "C" int32_t aiy_get_option(aiy_handle* h, int32_t option, int64_t* value)
     case AIY_OPT_GE_RESIDENT: *value = h->ge_resident; return AIY_OK;
     case AIY_OPT_GE_LOGSEC: *value = h->ge_logsec; return AIY_OK;
     case AIY_OPT_GE_EXTRAP_PERIOD: *value = h->ge_extrap_period; return AIY_OK;
+    case AIY_OPT_GE_ANDERSON: *value = h->ge_anderson; return AIY_OK;
     case AIY_OPT_GE_REBALANCE: *value = h->ge_rebalance; return AIY_OK;
     case AIY_OPT_CU_LIMIT: *value = h->cu_limit; return AIY_OK;
     case AIY_OPT_HIST_CLUSTER: *value = h->hist_cluster_cap; return AIY_OK;

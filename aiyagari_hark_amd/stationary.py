@@ -436,8 +436,11 @@ def solve_table2(cals=None, n_a=10000, aMin=0.001, aMax=50.0, aNestFac=2, r_tol=
     egm 1e-6 / hist 1e-10 and their sign is used only where |K_s - K_d| >= 5 % of K_d
     (else that r is evaluated again at the full tolerances).  The two bracket endpoints
     Brent's method starts from may be such loose evaluations (their sign is certain, their
-    value good to ~1e-6 relative); every later point is a full-tolerance evaluation, and
-    the root is still bracketed by the 5 % sign margin.  With loose bracketing the native
+    value good to ~1e-6 relative); Brent's points then run at an adaptive distribution
+    tolerance between hist_tol and the loose one (about 1e-9 of the smallest |K_s - K_d| / K_d
+    seen so far; a point whose |K_s - K_d| is not well above that evaluation's error is redone
+    at hist_tol), and the evaluation the search ends on is re-solved at hist_tol before its
+    K_s is reported; the root is still bracketed by the 5 % sign margin.  With loose bracketing the native
     search also brackets and runs Brent's method in log coordinates (log K_s/K_d against
     log(1/beta - 1 - r), where the excess supply is nearly linear; AIY_OPT_GE_LOGSEC,
     csrc/ge_search.h): the same root to r_tol in fewer evaluations.  extrapolate (native only;

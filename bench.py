@@ -61,6 +61,11 @@ N_TABLE2 = 24
 # kernel templates the legs' dominant launches are expected to use (PMC entries are matched
 # on them: a template the library no longer launches has no traffic figure)
 C1_PANEL_TEMPLATE = "sim_resident_kernel<512, 8, true, true"
+# configs[1]'s LDS-resident panel is not bound by HBM (its agents live in LDS; PMC traffic 0.40x
+# the 18 B per agent-period): its bound is the latency of the per-period work.  Floor: the
+# diagnostic build without the table lookups (draws, the partial-sum exchange, prices, the
+# asset update) at 6.2 us per period (tools/panel_variants.py, profiles/r02s_panel_variants.jsonl)
+C1_NO_LOOKUP_FLOOR_US = 6.2
 C3_PANEL_TEMPLATE = "sim_resident_kernel<1024, 4, false, true"
 EGM_C1_TEMPLATE = "egm_cycle_kernel<32, 28, false, 2"
 C4_TEMPLATE = "hist_pull_kernel<32, 512"
@@ -355,6 +360,7 @@ def configs1_leg(args, world, rank, dev):
     per_launch = st_per.value / max(1, st_n.value)
     panel_bytes = PANEL_BYTES_PER_AGENT * args.agents * per_launch
     panel_gbs = panel_bytes / max(1e-12, t_launch_ms * 1e-3) / 1e9
+    us_per_period = 1e3 * t_launch_ms / max(1.0, per_launch)
     t_egm_ms = egm_kernel_time(agent)
     egm_bytes = 32 * 28 * 15 * (args.grid + 1)
     egm_gbs = egm_bytes / (t_egm_ms * 1e-3) / 1e9
@@ -374,12 +380,20 @@ def configs1_leg(args, world, rank, dev):
                        "note": "the reference's market tolerance 0.01 stops this 1M-agent economy after 5 GE "
                                "iterations; at tolerance 1e-4 the same fixed point gives r = 4.092 % "
                                "(profiles/r02a_ks_tolerance_probe.jsonl, DESIGN.md §7)"},
-               roofline={"kernel": C1_PANEL_TEMPLATE + ">", "bound": "hbm", "achieved": panel_gbs,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": panel_gbs / HBM_PEAK_GBS,
+               roofline={"kernel": C1_PANEL_TEMPLATE + ">", "bound": "latency", "unit": "us/period",
+                         "achieved": us_per_period, "peak": C1_NO_LOOKUP_FLOOR_US,
+                         "frac": C1_NO_LOOKUP_FLOOR_US / max(1e-9, us_per_period),
+                         "bound_note": "agents resident in LDS (PMC traffic well below the 18 B per agent-period): "
+                                       "bound by the per-period latency chain, not HBM; peak = the no-lookup "
+                                       "diagnostic floor (every step of a period but the table lookups, "
+                                       "profiles/r02s_panel_variants.jsonl); frac = floor / achieved",
                          "traffic": p_traffic, **p_info, "algorithmic_bytes_per_launch": panel_bytes,
-                         "avg_launch_ms": t_launch_ms, "us_per_period": 1e3 * t_launch_ms / max(1.0, per_launch),
+                         "avg_launch_ms": t_launch_ms, "us_per_period": us_per_period,
                          "launch": f"one history: {per_launch:.0f} periods x {args.agents} agents",
-                         "launches_timed": st_n.value},
+                         "launches_timed": st_n.value,
+                         "hbm_units": {"achieved": panel_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": panel_gbs / HBM_PEAK_GBS,
+                                       "note": "18 B per agent-period (SURVEY.md §8d) / kernel time"}},
                roofline_egm={"kernel": EGM_C1_TEMPLATE + ">", "bound": "hbm", "achieved": egm_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": egm_gbs / HBM_PEAK_GBS, "traffic": e_traffic, **e_info,
                              "algorithmic_bytes_per_launch": egm_bytes, "avg_launch_ms": t_egm_ms},
@@ -759,6 +773,8 @@ def main():
                     help="AIY_OPT_HIST_PULL for the Table II / stress distribution solves (default: the library's)")
     ap.add_argument("--ge-rebalance", type=int, default=None,
                     help="AIY_OPT_GE_REBALANCE for the resident searches (default: the library's)")
+    ap.add_argument("--ge-anderson", type=int, default=None,
+                    help="AIY_OPT_GE_ANDERSON: EGM cycles between Anderson mixes in the resident search (0: off)")
     ap.add_argument("--hist-cluster", type=int, default=None,
                     help="AIY_OPT_HIST_CLUSTER: workgroups per calibration cluster cap (default the library's)")
     ap.add_argument("--ge-loose-hist", type=int, default=None,
@@ -780,7 +796,7 @@ def main():
     barrier(world)
     legs = set(args.legs.split(","))
     if (args.hist_pull is not None or args.ge_rebalance is not None or args.ge_loose_hist is not None or
-            args.hist_cluster is not None):
+            args.hist_cluster is not None or args.ge_anderson is not None):
         from aiyagari_hark_amd import _lib
         opts = {}
         if args.hist_pull is not None:
@@ -791,6 +807,8 @@ def main():
             opts[_lib.AIY_OPT_GE_LOOSE_HIST] = args.ge_loose_hist
         if args.hist_cluster is not None:
             opts[_lib.AIY_OPT_HIST_CLUSTER] = args.hist_cluster
+        if args.ge_anderson is not None:
+            opts[_lib.AIY_OPT_GE_ANDERSON] = args.ge_anderson
         _lib.handle(dev.index).set_options(opts)
     t2 = table2_leg(args, world, rank, dev)
     sweep_bytes = t2["hist_bytes_per_launch"] * t2["hist_launches_per_sweep"]
@@ -817,28 +835,30 @@ def main():
                                   + ("per GPU one device-resident launch, a cluster of workgroups per calibration "
                                      "running its whole root search" if t2["resident"] else
                                      "per GPU 3 independent root searches (own handle, stream, host thread)")},
+        # achieved / frac in SURVEY.md §8d's own units (28 B per histogram point per matvec, 32 B
+        # per (state, node) per EGM cycle); the same kernel time with the 24 B of
+        # BiCGSTAB iterate updates per point-matvec counted too is the secondary krylov_units
         "roofline": {"kernel": t2["kernel"], "bound": "hbm",
-                     "achieved": t2["hist_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
+                     "achieved": t2["s8d_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": t2["s8d_gbs"] / HBM_PEAK_GBS,
                      "traffic": t2_traffic, **t2_info,
-                     "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
+                     "algorithmic_bytes_per_launch": t2["s8d_bytes_per_launch"],
+                     "traffic_per_s8d_byte": (t2_traffic / t2["s8d_bytes_per_launch"]
+                                              if t2_traffic and t2["s8d_bytes_per_launch"] else None),
                      "avg_launch_ms": t2["hist_avg_launch_ms"],
                      "launch": ("one launch of the device-resident search (a sweep of the rank's calibrations "
                                 "runs as a few rebalancing launches, every K_s(r) evaluation of every root search "
-                                "in one of them): 52 B per state x node point per matvec of the distribution "
-                                "solves (28 B lottery push + mix, 24 B iterate updates) + 32 B per state x node "
-                                "per EGM cycle; traffic: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a profiled sweep "
-                                "per algorithmic byte, times this run's algorithmic bytes per launch" if t2["resident"] else
+                                "in one of them): 28 B per state x node point per matvec of the distribution "
+                                "solves (lottery push + mix, SURVEY.md §8d) + 32 B per state x node per EGM "
+                                "cycle; traffic: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of a profiled "
+                                "sweep, scaled to this run's launches" if t2["resident"] else
                                 "one K_s(r) evaluation of the rank's calibrations: every matvec of the solve "
-                                "(52 B per state x node point per matvec: 28 B lottery push + mix, 24 B iterate "
-                                "updates)"),
+                                "(28 B per state x node point per matvec, SURVEY.md §8d)"),
                      "kernel_time_share": t2["hist_kernel_ms_per_sweep"] / (1e3 * t2["seconds_per_sweep"]),
-                     # the same kernel time in SURVEY.md §8d's units (28 B per histogram point-iteration,
-                     # 32 B per EGM node-cycle; the 24 B of BiCGSTAB iterate updates not counted)
-                     "s8d_units": {"achieved": t2["s8d_gbs"], "frac": t2["s8d_gbs"] / HBM_PEAK_GBS,
-                                   "algorithmic_bytes_per_launch": t2["s8d_bytes_per_launch"],
-                                   "note": "28 B per state x node point per matvec + 32 B per state x node per EGM "
-                                           "cycle (SURVEY.md §8d)"},
+                     "krylov_units": {"achieved": t2["hist_gbs"], "frac": t2["hist_gbs"] / HBM_PEAK_GBS,
+                                      "algorithmic_bytes_per_launch": t2["hist_bytes_per_launch"],
+                                      "note": "52 B per state x node point per matvec (28 B lottery push + mix, 24 B "
+                                              "BiCGSTAB iterate updates) + 32 B per state x node per EGM cycle"},
                      # concurrent launches (independent groups) overlap: the device-level rate is the
                      # algorithmic bytes of a whole sweep over the sweep's wall time
                      "device_aggregate": {"achieved": sweep_bytes / t2["seconds_per_sweep"] / 1e9,

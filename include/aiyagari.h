@@ -360,7 +360,13 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     launch's calibrations have finished and relaunches the rest on
                                     the freed compute units (larger clusters); 0: one launch */
 #define AIY_OPT_GE_EXTRAP_PERIOD 13 /* device-resident GE search: EGM cycles between the geometric
-                                    extrapolation checks (4 .. 1024; default 32) */
+                                    extrapolation checks (4 .. 1024; default 32) when
+                                    AIY_OPT_GE_ANDERSON is 0 */
+#define AIY_OPT_GE_ANDERSON 23     /* device-resident GE search with egm_extrapolate: every p-th EGM cycle
+                                    (p in [5, 1024], default 12) the household iterate moves to the
+                                    type-II Anderson combination of the last 4 plain cycles (m = 3),
+                                    instead of the geometric extrapolation; the same fixed point and
+                                    HARK stopping rule (sup-norm change <= tol); 0: off */
 #define AIY_OPT_GE_LOGSEC 14      /* 1: with loose bracketing, while only K_s < K_d has been seen
                                     the next point is a secant of log(K_s / K_d) against
                                     log(1/beta - 1 - r) through the last two points (aimed 20 %
@@ -375,7 +381,11 @@ int32_t aiy_sim_block_periods(aiy_handle* h, const aiy_panel_batch* model, const
                                     deterministic run to run; 0: the push form.  S > 8 always pulls */
 #define AIY_OPT_GE_LOOSE_HIST 17   /* value v in [6, 14] (default 8): the loose-bracketing evaluations'
                                     distribution tolerance is 10^-v (their sign needs |K_s - K_d| >= 5 %
-                                    of K_d; the final bracket's evaluations use the full tolerance) */
+                                    of K_d).  Brent's evaluations run at an adaptive tolerance
+                                    between hist_tol and this one (ge_search.h ge_adapt_htol; an
+                                    evaluation whose |K_s - K_d| is not well above its error is
+                                    redone at hist_tol), and the evaluation the search ends on is
+                                    always re-solved at hist_tol before Ks_out is reported */
 #define AIY_OPT_RESIDENT_SHAPE_STREAM 18 /* workgroup shape (AIY_OPT_RESIDENT_SHAPE's values) of the resident
                                     panel's HBM-streaming form (agents beyond LDS, e.g. configs[3]);
                                     default 1 (1024 threads x 4 agents); -1: AIY_OPT_RESIDENT_SHAPE */
@@ -474,7 +484,10 @@ int64_t aiy_ge_stationary_work_bytes(int32_t n_cal, int32_t S, int32_t n_a);
  * per step, K_s(r) = sum(mass * a) of the stationary distribution (aiy_egm_solve ->
  * aiy_hist_lottery -> aiy_hist_solve) against K_d(r) = (alpha / (r + delta))^(1/(1-alpha)),
  * w(r) = (1 - alpha) K_d^alpha, R = 1 + r; the brackets move on the host.
- *   r_out, K_out (= K_d(r)), Ks_out (last K_s, may be NULL): HOST [n_cal];
+ *   r_out, K_out (= K_d(r)), Ks_out (the last evaluation's K_s, may be NULL): HOST [n_cal];
+ *   Ks_out always comes from a distribution solved to hist_tol: when the search ends on an
+ *   evaluation at the adaptive Brent tolerance (loose bracketing), that evaluation's
+ *   distribution is solved again at hist_tol from its mass before K_s is reported;
  *   steps_out: K_s evaluations; egm_cycles_out / hist_iters_out: their sums over steps and
  *   calibrations (may be NULL).  The converged tables, lottery and mass stay in `work`.
  * BLOCKING. */

@@ -173,6 +173,45 @@ def test_configs3_fullsize_streaming_panel_matches_oracle(c3, gpu):
 
 
 @pytest.mark.timeout(300)
+def test_configs3_fullsize_rccl_sharded_path_matches_oracle(c3, gpu):
+    """the path each rank of the 8-GPU configs[3] bench runs, at full size on
+    one rank.  With an RCCL communicator bound (here the library's own, one rank),
+    aiy_sim_periods runs per period ONE launch of the resident kernel's sharded streaming form
+    (kResSharded | kResPrices: every launch forms the previous period's prices from the
+    all-reduced sum in-kernel), then ncclAllReduce of the shard's sum (panel.hip sharded
+    branch).  n_local = n_total = 99 999 998 over the fixture's periods against the oracle:
+    labour counts exact, K / M history and sampled agents to 1e-12 (Aiyagari_Support.py:1868)."""
+    import ctypes
+
+    import bench
+    from aiyagari_hark_amd import _lib
+    fx, econ, agent, _ = c3
+    T = fx["periods"]
+    h = _lib.handle(gpu.index)
+    uid = ctypes.create_string_buffer(128)
+    assert h.lib.aiy_comm_unique_id(uid) == 0
+    h.check(h.lib.aiy_comm_init(h.h, uid, 1, 0), "aiy_comm_init")
+    try:
+        p, _ = bench.c3_panel(gpu, econ, agent, fx["agents"], T, 1, 0)
+        h.check(h.lib.aiy_panel_launch_stats(h.h, None, None, None, 1), "stats reset")
+        p.run(0, T, shock_mode="philox", seed=fx["seed"], ge_iter=fx["ge_iter"])
+        torch.cuda.synchronize()
+        ms, n, per = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        h.check(h.lib.aiy_panel_launch_stats(h.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(per), 1), "stats")
+    finally:
+        h.check(h.lib.aiy_comm_destroy(h.h), "aiy_comm_destroy")
+    # the sharded branch ran: one resident launch per period, none of them the single-rank
+    # (event-timed) multi-period launch
+    assert per.value == T and n.value == 0, (per.value, n.value)
+    idx = torch.as_tensor(fx["sample_idx"], device=gpu)
+    counts = torch.bincount(p.lab.long(), minlength=7).cpu().numpy()
+    _check_c3(fx, p.hist_A.cpu().numpy(), p.hist_M.cpu().numpy(), counts, p.a[idx].cpu().numpy(),
+              p.lab[idx].cpu().numpy(), T)
+    a = p.a.cpu().numpy()
+    assert abs(float(np.sum(a)) - fx["a_sum_final"]) / fx["a_sum_final"] < 1e-12
+
+
+@pytest.mark.timeout(300)
 def test_configs3_fullsize_two_step_shards_match_oracle(c3, gpu):
     """The sharded form of configs[3] at full size: two contiguous shards (split on agent
     pairs: the second starts at global index 50 000 000), each period aiy_sim_period_local on both

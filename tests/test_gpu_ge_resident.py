@@ -165,3 +165,45 @@ def test_pull_matvec_sweep_deterministic(gpu, n_a):
     assert np.all(a.status == 0) and np.all(b.status == 0)
     assert np.array_equal(a.r, b.r) and np.array_equal(a.K_supply, b.K_supply)
     assert np.max(np.abs(a.r - push.r)) <= 2e-7
+
+
+def test_final_ks_is_solved_at_hist_tol(gpu):
+    """bracketing evaluations run loose (egm 1e-6, hist 1e-8) and Brent's at an
+    adaptive distribution tolerance (up to the loose one), so a search that ENDS on such an
+    evaluation evaluates that r once more at egm_tol / hist_tol before K_s is reported.  A
+    coarse r_tol ends the searches while |K_s - K_d| is still large (during bracketing, or with
+    the adaptive tolerance above hist_tol); Ks_out must then equal K_s at the last evaluated r
+    solved cold at the full tolerances (the BiCGSTAB stopping rule leaves K ~4e5 tol relative
+    off, DESIGN.md §4c: ~4e-7 at 1e-12, ~4e-3 at the loose 1e-8)."""
+    import ctypes
+
+    from aiyagari_hark_amd import _lib
+    from aiyagari_hark_amd import setup_math as sm
+    from aiyagari_hark_amd.stationary import StationaryBatch, ge_stationary_native
+    cals = _cells(4)
+    aG = sm.make_grid_exp_mult(0.001, 50.0, 2000, 2)
+    b = StationaryBatch(cals, aG, device=gpu)
+    r, K, Ks, steps, cyc, its, status = ge_stationary_native(
+        b, "brent", 3e-4, 1e-8, 1e-12, 60, True, True, -1, secant=True, loose=True, extrapolate=True, resident=True)
+    assert np.all(status == 0)
+    h = _lib.handle(gpu.index)
+    ev = (ctypes.c_double * (len(cals) * 32 * 6))()
+    assert h.lib.aiy_ge_last_eval_log(h.h, ev, len(cals)) == len(cals)
+    ev = np.array(ev[:]).reshape(len(cals), 32, 6)
+    r_last, adaptive = [], []
+    for c in range(len(cals)):
+        rows = ev[c][ev[c][:, 0] != 0.0]
+        r_last.append(rows[-1, 0])
+        fmin = np.min(np.abs(rows[:-1, 1])) if len(rows) > 1 else np.inf
+        # a loose bracketing evaluation, or Brent's with ge_adapt_htol above hist_tol
+        adaptive.append(rows[-1, 4] == 1.0 or 1e-9 * fmin > 1e-12)
+    Kc, _, _ = StationaryBatch(cals, aG, device=gpu).capital_supply(np.array(r_last), egm_tol=1e-10, hist_tol=1e-12,
+                                                                    accel=-1)
+    rel = np.abs(Ks - Kc) / Kc
+    print(f"\nsteps {steps}; last r {np.round(100 * np.array(r_last), 5)}; loose / adaptive final evaluation {adaptive}; "
+          f"|Ks_out - K_s(hist_tol)| / K_s = {rel}")
+    assert any(adaptive), "no search ended on a loose evaluation: the test does not exercise the final pass"
+    # two solves at hist_tol = 1e-12 from different starts (the final pass warm, this one cold) stop
+    # at different points of the same rule: near 1/beta - 1 (cell 0, r = 4.14 %) the stopping rule
+    # leaves K a few 1e-6 relative off (DESIGN.md §2), against ~4e-3 for the loose evaluation
+    assert np.max(rel) <= 2e-5

@@ -642,25 +642,39 @@ def test_native_ge_search_equals_python_loop(gpu, method):
             assert np.max(np.abs(sec.r - py.r)) < 1e-7, (sec_on, loose_on, ex_on, grp, np.abs(sec.r - py.r))
 
 
-def test_distribution_solve_independent_of_launch_mates(gpu):
+@pytest.mark.parametrize("pull", [1, 0])
+def test_distribution_solve_independent_of_launch_mates(gpu, pull):
     """One calibration's BiCGSTAB distribution solve (aiy_hist_solve, one cluster per
-    calibration) gives the same K_s bit for bit whether it shares its launch with other
-    calibrations or runs alone, and with other work queued on the device: the clusters share
-    no data, and a solve's result depends only on its own inputs (tools/hist_determinism.py;
-    DESIGN.md §4f)."""
+    calibration) gives the same K_s whether it shares its launch with other calibrations or
+    runs alone, and with other work queued on the device: the clusters share no data, and a
+    solve's result depends only on its own inputs (tools/hist_determinism.py).
+    The pull form (AIY_OPT_HIST_PULL) has no atomics, so it is held bit for bit; the push
+    form's LDS atomics from different waves add to a boundary destination in an order the
+    hardware does not fix: a last-bit change in one matvec can move the Krylov path,
+    so it is held to the stopping rule's own accuracy (K within ~4e5 hist_tol relative of the
+    exact distribution, DESIGN.md §4c: 5e-7 here)."""
+    from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd import setup_math as sm
     from aiyagari_hark_amd.stationary import Calibration, StationaryBatch
     cals = [Calibration(LaborAR=0.6, LaborSD=0.2, CRRA=1.0), Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=5.0),
             Calibration(LaborAR=0.3, LaborSD=0.4, CRRA=3.0)]
     grid = sm.make_grid_exp_mult(0.001, 50.0, 300, 2)
     r = np.array([0.03, 0.02, float.fromhex("0x1.2a359f8a72972p-5")])
-    batch = StationaryBatch(cals, grid, device=gpu)
-    K3, _, it3 = batch.capital_supply(r, accel=-1)
-    assert np.all(np.isfinite(K3)) and np.all(it3 > 0)
-    x = torch.randn(2048, 2048, device=gpu)
-    for c in range(len(cals)):
-        y = torch.tanh(x @ x * 1e-3)   # queued ahead of the solve's launches
-        alone = StationaryBatch([cals[c]], grid, device=gpu)
-        K1, _, _ = alone.capital_supply(r[c:c + 1], accel=-1)
-        assert float(K1[0]).hex() == float(K3[c]).hex(), (c, K1[0], K3[c])
-    assert torch.isfinite(y).all()
+    h = _lib.handle(gpu.index)
+    prev = h.set_options({_lib.AIY_OPT_HIST_PULL: pull})
+    try:
+        batch = StationaryBatch(cals, grid, device=gpu)
+        K3, _, it3 = batch.capital_supply(r, accel=-1)
+        assert np.all(np.isfinite(K3)) and np.all(it3 > 0)
+        x = torch.randn(2048, 2048, device=gpu)
+        for c in range(len(cals)):
+            y = torch.tanh(x @ x * 1e-3)   # queued ahead of the solve's launches
+            alone = StationaryBatch([cals[c]], grid, device=gpu)
+            K1, _, _ = alone.capital_supply(r[c:c + 1], accel=-1)
+            if pull:
+                assert float(K1[0]).hex() == float(K3[c]).hex(), (c, K1[0], K3[c])
+            else:
+                assert abs(K1[0] - K3[c]) <= 5e-7 * abs(K3[c]), (c, K1[0], K3[c])
+        assert torch.isfinite(y).all()
+    finally:
+        h.set_options(prev)

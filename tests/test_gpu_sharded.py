@@ -67,11 +67,14 @@ def _check(got, ref):
     assert np.max(np.abs(hM - rhM) / np.abs(rhM)) < 1e-13
 
 
-@pytest.mark.parametrize("mode", ["philox", "numpy"])
-def test_two_step_shards_equal_unsharded(gpu, mode):
-    """Two shards in one process (odd split: the second shard starts at an odd global
-    index, so its Philox pairs straddle the shard boundary), summed between the two
-    library steps, against the unsharded panel."""
+@pytest.mark.parametrize("mode,split", [("philox", "pairs"), ("numpy", "pairs"), ("philox", "odd")])
+def test_two_step_shards_equal_unsharded(gpu, mode, split):
+    """Two shards in one process, summed between the two library steps, against the unsharded
+    panel.  split "pairs": parallel.shard_range, which splits on agent pairs (offsets 0 and
+    100 002 for N = 200 001: every shard takes the resident kernel); split "odd": hand-built
+    shards (0, 100 001) and (100 001, 100 000) whose boundary cuts a Philox pair (2k, 2k + 1),
+    so the second shard runs the per-period sim_period_kernel fallback of aiy_sim_period_local
+    (ADVICE r5)."""
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.parallel import shard_range
     fx = _fixture()
@@ -81,8 +84,9 @@ def test_two_step_shards_equal_unsharded(gpu, mode):
     ref = _unsharded(gpu, fx, N, T, lab0, seed, U)
     h = _lib.handle(gpu.index)
     shards = []
-    for r in range(2):
-        off, nl = shard_range(N, 2, r)
+    ranges = [shard_range(N, 2, r) for r in range(2)] if split == "pairs" else [(0, 100_001), (100_001, 100_000)]
+    assert ranges[1][0] % 2 == (0 if split == "pairs" else 1)
+    for off, nl in ranges:
         p = _panel(gpu, fx, nl, T, offset=off, n_total=N)
         _reset(p, fx, lab0[off:off + nl])
         shards.append((off, nl, p))

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--logsec", type=int, default=-1, help="AIY_OPT_GE_LOGSEC (-1: default)")
     ap.add_argument("--loose-hist", type=int, default=-1, help="AIY_OPT_GE_LOOSE_HIST (-1: default)")
     ap.add_argument("--stress", action="store_true", help="configs[4]'s 3 cells (25 states) instead of Table II")
+    ap.add_argument("--all-evals", action="store_true", help="print every calibration's evaluation log")
     args = ap.parse_args()
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.stationary import Calibration, solve_table2, table2_calibrations
@@ -91,10 +92,11 @@ def main():
             out["evaluations"] = [[dict(r=float(x[0]), f_rel=float(x[1]), egm_cycles=int(x[2]), matvecs=int(x[3]),
                                         loose=int(x[4]), us=round(float(x[5]), 1)) for x in e[c] if x[2] > 0]
                                   for c in range(ne)]
-            for c in ((0, 1, 2) if args.stress else (0, 11, 23)):
+            for c in (range(ne) if args.all_evals else ((0, 1, 2) if args.stress else (0, 11, 23))):
                 if c < ne:
                     print(f"[evals] cell {c}: " + "; ".join(f"r={x['r']:.6f} f={x['f_rel']:+.1e} cyc={x['egm_cycles']} "
-                                                            f"mv={x['matvecs']}{' L' if x['loose'] else ''}"
+                                                            f"mv={x['matvecs']}{' L' if x['loose'] else ''} "
+                                                            f"{x['us']:.0f}us"
                                                             for x in out["evaluations"][c]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 
