@@ -30,6 +30,7 @@ extern "C" int32_t aiy_destroy(aiy_handle* h) {
   if (h->d_dist) (void)hipFree(h->d_dist);
   if (h->d_last) (void)hipFree(h->d_last);
   if (h->d_egm_hint) (void)hipFree(h->d_egm_hint);
+  if (h->d_egm_aa) (void)hipFree(h->d_egm_aa);
   if (h->h_dist) (void)hipHostFree(h->h_dist);
   if (h->h_last) (void)hipHostFree(h->h_last);
   if (h->d_partials) (void)hipFree(h->d_partials);

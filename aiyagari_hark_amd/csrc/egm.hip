@@ -657,6 +657,86 @@ __global__ void egm_extrap_kernel(long long per, int n_cal, const double* __rest
   }
 }
 
+// Periodic Anderson mixing of the host-driven stationary EGM solve (aiy_ge_stationary's household
+// solves with egm_extrapolate, n_M = 1; AIY_OPT_GE_ANDERSON = p: every p-th cycle, m = 3), the
+// same mixing as the device-resident search (ge_resident.hip): from the c tables w0 .. w4 of the
+// last five plain cycles, g_i = w_{i+1} - w_i, dG_i = g_{i+1} - g_i, dF_i = w_{i+2} - w_{i+1},
+// gamma = argmin |g_3 - dG gamma|, and the next iterate w4 - dF gamma (m = a + c; the (1e-7, 1e-7)
+// node fixed).  Gram partials per (calibration, block) in a fixed order; the host sums the blocks
+// in order and solves each calibration's 3 x 3 system.
+constexpr int kEgmAaBlocks = 64;
+__global__ __launch_bounds__(256) void egm_aa_gram_kernel(long long per, const double* __restrict__ ring,
+                                                          long long buf, int c0, double* __restrict__ part) {
+  // ring: 5 slots of [n_cal][per]; slot (c0 + i) % 5 holds w_i
+  const int cal = blockIdx.y;
+  const double* W[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) W[i] = ring + (size_t)((c0 + i) % 5) * buf + (size_t)cal * per;
+  double acc[9];
+#pragma unroll
+  for (int v = 0; v < 9; ++v) acc[v] = 0.0;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (long long)gridDim.x * blockDim.x) {
+    const double w0 = W[0][q], w1 = W[1][q], w2 = W[2][q], w3 = W[3][q], w4 = W[4][q];
+    const double g0 = w1 - w0, g1 = w2 - w1, g2 = w3 - w2, g3 = w4 - w3;
+    const double d0 = g1 - g0, d1 = g2 - g1, d2 = g3 - g2;
+    acc[0] += d0 * d0; acc[1] += d0 * d1; acc[2] += d0 * d2;
+    acc[3] += d1 * d1; acc[4] += d1 * d2; acc[5] += d2 * d2;
+    acc[6] += d0 * g3; acc[7] += d1 * g3; acc[8] += d2 * g3;
+  }
+  __shared__ double s_w[9][256 / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int v = 0; v < 9; ++v) {
+    const double x = wave_sum_fixed(acc[v]);
+    if (lane == 0) s_w[v][wid] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    double x = 0.0;
+    for (int q = 0; q < 256 / kWave; ++q) x += s_w[threadIdx.x][q];
+    part[((size_t)cal * gridDim.x + blockIdx.x) * 9 + threadIdx.x] = x;
+  }
+}
+
+__global__ void egm_aa_mix_kernel(long long per, int n_a, const double* __restrict__ ring, long long buf, int c0,
+                                  const double* __restrict__ gam, const double* __restrict__ a_grid,
+                                  double* __restrict__ out_m, double* __restrict__ out_c) {
+  const int cal = blockIdx.y;
+  const double* g = gam + (size_t)cal * 4;
+  if (g[3] == 0.0) return;   // this calibration is not mixed (converged, or a degenerate system)
+  const double c0g = g[0], c1g = g[1], c2g = g[2];
+  const double* W1 = ring + (size_t)((c0 + 1) % 5) * buf + (size_t)cal * per;
+  const double* W2 = ring + (size_t)((c0 + 2) % 5) * buf + (size_t)cal * per;
+  const double* W3 = ring + (size_t)((c0 + 3) % 5) * buf + (size_t)cal * per;
+  const double* W4 = ring + (size_t)((c0 + 4) % 5) * buf + (size_t)cal * per;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(q % (n_a + 1));
+    if (j == 0) continue;   // the (1e-7, 1e-7) node
+    const double w1 = W1[q], w2 = W2[q], w3 = W3[q], w4 = W4[q];
+    const double cn = w4 - ((c0g * (w2 - w1) + c1g * (w3 - w2)) + c2g * (w4 - w3));
+    out_c[(size_t)cal * per + q] = cn;
+    out_m[(size_t)cal * per + q] = a_grid[(size_t)cal * n_a + j - 1] + cn;   // AS:1499
+  }
+}
+
+// gamma of one calibration from its summed Gram entries (the resident search's Cholesky, same
+// regularisation); false: degenerate or non-finite (no mix)
+static bool egm_aa_solve(const double* gs, double* gam) {
+  double a00 = gs[0], a01 = gs[1], a02 = gs[2], a11 = gs[3], a12 = gs[4], a22 = gs[5];
+  const double b0 = gs[6], b1 = gs[7], b2 = gs[8];
+  const double reg = 1e-12 * (a00 + a11 + a22);
+  if (!(reg > 0.0)) return false;
+  a00 += reg; a11 += reg; a22 += reg;
+  const double l00 = std::sqrt(a00), l10 = a01 / l00, l20 = a02 / l00;
+  const double l11 = std::sqrt(a11 - l10 * l10), l21 = (a12 - l20 * l10) / l11;
+  const double l22 = std::sqrt(a22 - l20 * l20 - l21 * l21);
+  const double y0 = b0 / l00, y1 = (b1 - l10 * y0) / l11, y2 = (b2 - l20 * y0 - l21 * y1) / l22;
+  gam[2] = y2 / l22;
+  gam[1] = (y1 - l21 * gam[2]) / l11;
+  gam[0] = (y0 - l10 * gam[1] - l20 * gam[2]) / l00;
+  return std::isfinite(gam[0]) && std::isfinite(gam[1]) && std::isfinite(gam[2]);
+}
+
 int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_egm_inputs* in, double tol,
                               int32_t max_cycles, int32_t chunk, const double* m_init, const double* c_init,
                               double* work_m, double* work_c, double* m_out, double* c_out, int32_t* cycles_out,
@@ -690,6 +770,27 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
   const int last_allowed = max_cycles + 1;  // HARK: go = d > tol and completed < max_cycles
   int next = 1;
   const bool extrap = h->egm_extrap != 0;
+  // Anderson mixing instead of the geometric extrapolation (stationary solves, n_M = 1): the
+  // host check runs every p cycles, the c tables of each chunk's last five cycles are kept
+  const bool aa = extrap && h->ge_anderson > 0 && dims->n_M == 1;
+  double* ring = nullptr;
+  double* d_part = nullptr;
+  double* d_gam = nullptr;
+  if (aa) {
+    chunk = h->ge_anderson;
+    const size_t need = 5 * buf + (size_t)n_cal * kEgmAaBlocks * 9 + (size_t)n_cal * 4;
+    if (need > h->egm_aa_cap) {
+      if (h->d_egm_aa) (void)hipFree(h->d_egm_aa);
+      h->d_egm_aa = nullptr;
+      h->egm_aa_cap = 0;
+      AIY_HIP(h, hipMalloc((void**)&h->d_egm_aa, need * sizeof(double)));
+      h->egm_aa_cap = need;
+    }
+    ring = h->d_egm_aa;
+    d_part = ring + 5 * buf;
+    d_gam = d_part + (size_t)n_cal * kEgmAaBlocks * 9;
+  }
+  std::vector<double> h_part(aa ? (size_t)n_cal * kEgmAaBlocks * 9 : 0), h_gam(aa ? (size_t)n_cal * 4 : 0);
   std::vector<double> lam_prev(n_cal, -1.0);
   std::vector<char> moved(n_cal, 0);
   double* hf = reinterpret_cast<double*>(h->h_dist + (size_t)kSlots * n_cal);
@@ -702,21 +803,59 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
       const double* cn = term ? nullptr : work_c + ((cyc - 1) & 1) * buf;
       launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, hints, cyc, h->d_dist, h->d_last,
                    tol, st);
+      if (aa && cyc >= end - 5)   // the chunk's last five outputs (c) for the mix
+        AIY_HIP(h, hipMemcpyAsync(ring + (size_t)(cyc % 5) * buf, work_c + (cyc & 1) * buf, buf * sizeof(double),
+                                  hipMemcpyDeviceToDevice, st));
     }
     AIY_CHECK_LAUNCH(h);
     AIY_HIP(h, hipMemcpyAsync(h->h_last, h->d_last, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipMemcpyAsync(h->h_dist, h->d_dist, sizeof(unsigned long long) * kSlots * n_cal, hipMemcpyDeviceToHost, st));
     AIY_HIP(h, hipStreamSynchronize(st));
     bool all = true;
+    std::vector<char> conv(n_cal, 0);
     for (int c = 0; c < n_cal; ++c) {
       const int last = h->h_last[c];
       const double d = slot_max(h->h_dist + (size_t)c * kSlots, last);
-      const bool conv = (last >= 2 && !(d > tol_of(c))) || last >= last_allowed;
-      all = all && conv;
+      conv[c] = (last >= 2 && !(d > tol_of(c))) || last >= last_allowed;
+      all = all && conv[c];
     }
+    const int start = next;
     next = end;
     if (all || next > last_allowed) break;
-    if (extrap) {
+    if (aa) {
+      const int L = end - 1;   // the last launched cycle: w4 (its tables in slot L & 1)
+      bool any = false;
+      // (a calibration still running at L, whose last five cycles all ran in this chunk)
+      auto mixable = [&](int c) { return !conv[c] && h->h_last[c] == L && end - start >= 5; };
+      for (int c = 0; c < n_cal; ++c) any = any || mixable(c);
+      if (any) {
+        const long long per = (long long)per_cal;
+        hipLaunchKernelGGL(egm_aa_gram_kernel, dim3(kEgmAaBlocks, n_cal), dim3(256), 0, st, per, ring, (long long)buf,
+                           L - 4, d_part);
+        AIY_CHECK_LAUNCH(h);
+        AIY_HIP(h, hipMemcpyAsync(h_part.data(), d_part, h_part.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        AIY_HIP(h, hipStreamSynchronize(st));
+        bool mix = false;
+        for (int c = 0; c < n_cal; ++c) {
+          double gs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+          for (int b = 0; b < kEgmAaBlocks; ++b)
+            for (int v = 0; v < 9; ++v) gs[v] += h_part[((size_t)c * kEgmAaBlocks + b) * 9 + v];
+          double* g = &h_gam[(size_t)c * 4];
+          g[3] = 0.0;
+          if (mixable(c) && egm_aa_solve(gs, g)) {
+            g[3] = 1.0;
+            moved[c] = 1;
+            mix = true;
+          }
+        }
+        if (mix) {
+          AIY_HIP(h, hipMemcpyAsync(d_gam, h_gam.data(), h_gam.size() * sizeof(double), hipMemcpyHostToDevice, st));
+          hipLaunchKernelGGL(egm_aa_mix_kernel, dim3(256, n_cal), dim3(256), 0, st, per, dims->n_a, ring,
+                             (long long)buf, L - 4, d_gam, A.a_grid, work_m + (L & 1) * buf, work_c + (L & 1) * buf);
+          AIY_CHECK_LAUNCH(h);
+        }
+      }
+    } else if (extrap) {
       const int L = end - 1;   // the last launched cycle; its tables sit in slot L & 1
       bool any = false;
       for (int c = 0; c < n_cal; ++c) {

@@ -21,6 +21,8 @@ struct aiy_handle {
   int* d_last = nullptr;
   size_t egm_cap = 0;
   int* d_egm_hint = nullptr;         // EGM row hints [work item][rows x S] (egm.hip)
+  double* d_egm_aa = nullptr;        // Anderson mixing of the host-driven EGM solve (egm.hip): the c
+  size_t egm_aa_cap = 0;             //   tables of the last 5 cycles + Gram partials + gamma (doubles)
   size_t egm_hint_cap = 0;           // ints
   unsigned long long egm_hint_sig = ~0ull;   // shape the hints belong to
   // host pinned mirrors

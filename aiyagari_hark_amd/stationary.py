@@ -334,7 +334,7 @@ def ge_stationary_native(b, method, r_tol, egm_tol, hist_tol, max_steps, warm_hi
 
 _GROUP_CTX = {}   # (device, group) -> (library handle, torch stream), reused across sweeps
 _GROUP_CARRY_OPTIONS = (_lib.AIY_OPT_GE_LOGSEC, _lib.AIY_OPT_GE_REBALANCE, _lib.AIY_OPT_GE_EXTRAP_PERIOD,
-                        _lib.AIY_OPT_HIST_PULL, _lib.AIY_OPT_GE_LOOSE_HIST)
+                        _lib.AIY_OPT_HIST_PULL, _lib.AIY_OPT_GE_LOOSE_HIST, _lib.AIY_OPT_GE_ANDERSON)
 
 
 def _close_groups():

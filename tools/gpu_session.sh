@@ -102,6 +102,8 @@ for step in "$@"; do
             for pp in ${AAP:-0}; do run abaa_p${pp}_$rep 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-anderson $pp; done
             for v in ${VARIANTS:-}; do run abaa_${v}_$rep 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline; done
           done ;;
+    abc4aa) for rep in 1 2; do run abc4aa_def_$rep 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline && run abc4aa_p0_$rep 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline --ge-anderson 0; done ;;
+    c4size) run c4size 600 $PYT -s tests/test_gpu_benchsize.py::test_stress_ge_matches_oracle_fullsize ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
