@@ -117,7 +117,7 @@ def main():
     if os.environ.get("OPTS"):
         opts_all = opts_var = [tuple(o) for o in json.loads(os.environ["OPTS"])]
     for name, lib in libs:
-        opts = opts_all if lib is None else opts_var
+        opts = opts_all if (lib is None or os.environ.get("OPTS")) else opts_var
         rc = subprocess.run([sys.executable, __file__, "--child", lib or "-", json.dumps(opts)], timeout=300).returncode
         if rc != 0:
             print(json.dumps(dict(lib=name, error=rc)), flush=True)
