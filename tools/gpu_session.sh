@@ -107,6 +107,7 @@ for step in "$@"; do
     abq) for rep in 1 2; do for q in ${QS:-45 65}; do run abq_q${q}_$rep 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance $q ${QEXTRA:-}; done; done ;;
     ph24) run ph24 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 24 --rebalance 0 ;;
     c3shape) run c3shape 600 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200],[1,0,3,0,200]]' FUSE=0 AIY_VARIANTS=c3pre=aiyagari_hark_amd/lib/variants/libaiyagari_c3pre.so python -u tools/panel_variants.py ;;
+    c3ph) run c3ph 600 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
