@@ -698,9 +698,10 @@ __global__ __launch_bounds__(256) void egm_aa_gram_kernel(long long per, const d
   }
 }
 
-__global__ void egm_aa_mix_kernel(long long per, int n_a, const double* __restrict__ ring, long long buf, int c0,
+// (out_c is cycle c0 + 4's ring slot itself: no restrict on ring / out_c)
+__global__ void egm_aa_mix_kernel(long long per, int n_a, const double* ring, long long buf, int c0,
                                   const double* __restrict__ gam, const double* __restrict__ a_grid,
-                                  double* __restrict__ out_m, double* __restrict__ out_c) {
+                                  double* __restrict__ out_m, double* out_c) {
   const int cal = blockIdx.y;
   const double* g = gam + (size_t)cal * 4;
   if (g[3] == 0.0) return;   // this calibration is not mixed (converged, or a degenerate system)
@@ -791,6 +792,9 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
     d_gam = d_part + (size_t)n_cal * kEgmAaBlocks * 9;
   }
   std::vector<double> h_part(aa ? (size_t)n_cal * kEgmAaBlocks * 9 : 0), h_gam(aa ? (size_t)n_cal * 4 : 0);
+  // where each cycle's c output lives (cycle 0: the caller's start in ping-pong slot 0)
+  std::vector<double*> cloc((size_t)last_allowed + 2, nullptr);
+  cloc[0] = work_c;
   std::vector<double> lam_prev(n_cal, -1.0);
   std::vector<char> moved(n_cal, 0);
   double* hf = reinterpret_cast<double*>(h->h_dist + (size_t)kSlots * n_cal);
@@ -800,12 +804,12 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
     for (int cyc = next; cyc < end; ++cyc) {
       const bool term = cyc == 1 && !warm;
       const double* mn = term ? nullptr : work_m + ((cyc - 1) & 1) * buf;
-      const double* cn = term ? nullptr : work_c + ((cyc - 1) & 1) * buf;
-      launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, work_c + (cyc & 1) * buf, hints, cyc, h->d_dist, h->d_last,
-                   tol, st);
-      if (aa && cyc >= end - 5)   // the chunk's last five outputs (c) for the mix
-        AIY_HIP(h, hipMemcpyAsync(ring + (size_t)(cyc % 5) * buf, work_c + (cyc & 1) * buf, buf * sizeof(double),
-                                  hipMemcpyDeviceToDevice, st));
+      const double* cn = term ? nullptr : cloc[cyc - 1];
+      // the chunk's last five c outputs go straight into the Anderson ring (no copies); a
+      // converged calibration's cycles write nothing, so its tables stay where they were written
+      double* co = (aa && cyc >= end - 5) ? ring + (size_t)(cyc % 5) * buf : work_c + (cyc & 1) * buf;
+      cloc[cyc] = co;
+      launch_cycle(A, mn, cn, work_m + (cyc & 1) * buf, co, hints, cyc, h->d_dist, h->d_last, tol, st);
     }
     AIY_CHECK_LAUNCH(h);
     AIY_HIP(h, hipMemcpyAsync(h->h_last, h->d_last, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
@@ -850,8 +854,9 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
         }
         if (mix) {
           AIY_HIP(h, hipMemcpyAsync(d_gam, h_gam.data(), h_gam.size() * sizeof(double), hipMemcpyHostToDevice, st));
+          // (in place over cycle L's c in the ring: each element is read before it is written)
           hipLaunchKernelGGL(egm_aa_mix_kernel, dim3(256, n_cal), dim3(256), 0, st, per, dims->n_a, ring,
-                             (long long)buf, L - 4, d_gam, A.a_grid, work_m + (L & 1) * buf, work_c + (L & 1) * buf);
+                             (long long)buf, L - 4, d_gam, A.a_grid, work_m + (L & 1) * buf, cloc[L]);
           AIY_CHECK_LAUNCH(h);
         }
       }
@@ -909,8 +914,7 @@ int32_t aiy_egm_solve_impl(aiy_handle* h, const aiy_egm_dims* dims, const aiy_eg
     const size_t off = (size_t)c * per_cal;
     AIY_HIP(h, hipMemcpyAsync(m_out + off, work_m + (last & 1) * buf + off, per_cal * sizeof(double),
                               hipMemcpyDeviceToDevice, st));
-    AIY_HIP(h, hipMemcpyAsync(c_out + off, work_c + (last & 1) * buf + off, per_cal * sizeof(double),
-                              hipMemcpyDeviceToDevice, st));
+    AIY_HIP(h, hipMemcpyAsync(c_out + off, cloc[last] + off, per_cal * sizeof(double), hipMemcpyDeviceToDevice, st));
   }
   AIY_HIP(h, hipStreamSynchronize(st));
   return AIY_OK;

@@ -108,6 +108,7 @@ for step in "$@"; do
     ph24) run ph24 300 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/ge_resident_profile.py --modes resident --reps 1 --cells 24 --rebalance 0 ;;
     c3shape) run c3shape 600 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200],[1,0,3,0,200]]' FUSE=0 AIY_VARIANTS=c3pre=aiyagari_hark_amd/lib/variants/libaiyagari_c3pre.so python -u tools/panel_variants.py ;;
     c3ph) run c3ph 600 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=phases=aiyagari_hark_amd/lib/variants/libaiyagari_phases.so python -u tools/panel_variants.py ;;
+    c3dg) run c3dg 600 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=dg10=aiyagari_hark_amd/lib/variants/libaiyagari_dg10.so,dg16=aiyagari_hark_amd/lib/variants/libaiyagari_dg16.so python -u tools/panel_variants.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
