@@ -33,6 +33,7 @@ namespace aiy {
 
 constexpr int kHpHeavy = 64;   // sources of one destination above which its wave sums them
 constexpr int kHpUnroll = 4;   // wave strides of a heavy sum with their loads in flight together
+constexpr int kHpRunLane = 32;   // inverse-lottery runs longer than this are stored by the whole wave
 
 struct HpArgs {
   int G, S, n_a, w, j0, j1;
@@ -133,22 +134,50 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   // a lottery written in this launch (the resident GE search): every workgroup's entries are
   // in memory before the neighbour's column j0 - 1 is read
   if (r.lottery_fresh && !barrier()) return -1;
-  for (int q = tid; q < S * n_own; q += TH) {
-    const int s = q / n_own, j = j0 + (q - s * n_own);
-    const int l = lo_at(s, j);
-    const int lp = j > 0 ? lo_at(s, j - 1) : -1;
-    // only a monotone lottery inside the grid is scattered (anything else: error 2, the caller
-    // falls back); the loops never index outside the row
-    const bool ok = l >= 0 && l <= n_a - 2 && lp >= -1 && lp <= l;
-    if (!ok) {
-      bad = 2u;
-      continue;
+  // A(d) = j for d in (lo_{j-1}, lo_j], and n_a past lo_{n_a-1}: a run per source.  A source
+  // can own a long run (the borrowing-constrained agent of a high income state saves past
+  // ~30 000 of 50 000 nodes at configs[4]), which one lane stored serially in ~1.3 ms: runs
+  // longer than kHpRunLane are stored by the lane's whole wave
+  auto fill_run = [&](int s, int b, int e, int v) {   // A(d) = v for d in [b, e] of row s
+    const bool wide = e - b >= kHpRunLane;
+    if (!wide)
+      for (int d = b; d <= e; ++d)
+        __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long wm = __ballot(wide);
+    while (wm) {   // wave-uniform
+      const int h = __builtin_ctzll(wm);
+      wm &= wm - 1ull;
+      const int sh = __builtin_amdgcn_readlane(s, h), bh = __builtin_amdgcn_readlane(b, h),
+                eh = __builtin_amdgcn_readlane(e, h), vh = __builtin_amdgcn_readlane(v, h);
+      for (int d = bh + lane; d <= eh; d += kWave)
+        __hip_atomic_store(to_global(&A[(size_t)sh * n1 + d]), vh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (int d = lp + 1; d <= l; ++d)
-      __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (j == n_a - 1)
-      for (int d = l + 1; d <= n_a; ++d)
-        __hip_atomic_store(to_global(&A[(size_t)s * n1 + d]), n_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int q0 = 0; q0 < S * n_own; q0 += TH) {   // uniform trip count (the wave fills need every lane)
+    const int q = q0 + tid;
+    int s = 0, rb = 0, re = -1, rv = 0, tb = 0, te = -1;   // empty runs
+    if (q < S * n_own) {
+      s = q / n_own;
+      const int j = j0 + (q - s * n_own);
+      const int l = lo_at(s, j);
+      const int lp = j > 0 ? lo_at(s, j - 1) : -1;
+      // only a monotone lottery inside the grid is scattered (anything else: error 2, the caller
+      // falls back); the runs never leave the row
+      const bool ok = l >= 0 && l <= n_a - 2 && lp >= -1 && lp <= l;
+      if (!ok) {
+        bad = 2u;
+      } else {
+        rb = lp + 1;
+        re = l;
+        rv = j;
+        if (j == n_a - 1) {
+          tb = l + 1;
+          te = n_a;
+        }
+      }
+    }
+    fill_run(s, rb, re, rv);
+    fill_run(s, tb, te, n_a);
   }
   if (bad) __hip_atomic_store(to_global(err), bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // exported prefix [j0, ex0) (lo < j0) and suffix [ex1, j1) (lo + 1 >= j1) of each row
