@@ -22,6 +22,7 @@ constexpr int kHcRedRec = 16;                     // 8-byte words per (parity, w
 
 struct HcRun {
   int n_cal, cal0, S, n_a, G, nj, cap;   // cap: doubles of the span buffer / one slab
+  int cw;                 // pull form: columns of one matvec chunk (hist_pull_plan)
   const int* lo;          // [n_cal][S][n_a]
   const double* wlo;      // [n_cal][S][n_a]
   const double* P;        // [n_cal][S][S]
@@ -141,7 +142,9 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
 const void* hist_bicg_pick(int S, int smax, int kc, int* smax_k, bool pull = false);
 // pull form (hist_pull.h) for S > 8: the kernel, and its dynamic LDS for n_own columns
 const void* hist_pull_pick(int S);
-size_t hist_pull_lds(int S, int n_own);
+// pull form: the column chunk of a matvec (fewest item rounds + mix passes whose LDS fits
+// `budget`) and its dynamic LDS bytes; false when even one-column chunks do not fit
+bool hist_pull_plan(int S, int n_own, size_t budget, int* cw, size_t* lds);
 constexpr int kHpTH = 512;
 
 }  // namespace aiy

@@ -112,6 +112,7 @@ __global__ __launch_bounds__(TH) void hist_pull_kernel(HcRun r) {
   a.G = G; a.S = S; a.n_a = n_a; a.w = w;
   a.j0 = w * r.nj;
   a.j1 = min(a.j0 + r.nj, n_a);
+  a.cw = r.cw;
   a.LO = to_global(r.lo + row0 * n_a);
   a.WL = to_global(r.wlo + row0 * n_a);
   a.lottery_fresh = false;   // written by the lottery launch before this one
@@ -140,7 +141,24 @@ const void* hist_pull_pick(int S) {
   if (S <= 32) return reinterpret_cast<const void*>(hist_pull_kernel<32, kHpTH>);
   return nullptr;
 }
-size_t hist_pull_lds(int S, int n_own) { return hp_lds_a_bytes<1>(n_own) * (size_t)S; }
+bool hist_pull_plan(int S, int n_own, size_t budget, int* cw, size_t* lds) {
+  const int ng = (S + kHpGrp - 1) / kHpGrp;
+  long best = -1;
+  for (int nch = 1; nch <= n_own; ++nch) {
+    const int c = (n_own + nch - 1) / nch;
+    const size_t b = (hp_lds_bytes(S, n_own, c) + 255) / 256 * 256;
+    if (b > budget) continue;
+    // latency rounds per matvec: the chunks' item rounds and mix passes
+    const long cost = (long)nch * (((long)ng * c + kHpTH - 1) / kHpTH + (c + kHpTH - 1) / kHpTH);
+    if (best < 0 || cost < best) {
+      best = cost;
+      *cw = c;
+      *lds = b;
+    }
+    if (best >= 0 && (long)(nch + 1) * 2 > best) break;   // every chunk costs >= 2 rounds
+  }
+  return best >= 0;
+}
 
 template <int SMAX, int KC, int TH, bool PULL = false>
 static const void* hk_fn() {

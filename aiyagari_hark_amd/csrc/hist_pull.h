@@ -34,9 +34,11 @@ namespace aiy {
 constexpr int kHpHeavy = 64;   // sources of one destination above which its wave sums them
 constexpr int kHpUnroll = 4;   // wave strides of a heavy sum with their loads in flight together
 constexpr int kHpRunLane = 32;   // inverse-lottery runs longer than this are stored by the whole wave
+constexpr int kHpGrp = 5;      // income states of one pull item
 
 struct HpArgs {
   int G, S, n_a, w, j0, j1;
+  int cw;                     // columns of one matvec chunk (the row sums of a chunk sit in LDS)
   gptr<const int> LO;         // [S][n_a] lottery index
   gptr<const double> WL;      // [S][n_a] lottery weight on lo
   bool lottery_fresh;         // LO / WL written in this launch by other workgroups (sc1 loads)
@@ -54,7 +56,8 @@ struct HpArgs {
 };
 
 // LDS of the solve: P, the staged inverse lottery of the own destinations d in [j0 - 1, j1]
-// (row stride n_own + 2), the exported prefix / suffix bounds, reduction partials.
+// (row stride n_own + 2) followed by a chunk's row sums ([S][cw] doubles, hp_lds_bytes), the
+// exported prefix / suffix bounds, reduction partials.
 template <int SMAX, int TH>
 struct HpShared {
   double* s_P;                     // [SMAX][SMAX]
@@ -65,9 +68,11 @@ struct HpShared {
   int* s_flag;
   int* s_stop;
 };
-template <int SMAX>
-__host__ __device__ constexpr size_t hp_lds_a_bytes(int n_own) {
-  return (size_t)SMAX * (size_t)(n_own + 2) * sizeof(int);
+__host__ __device__ constexpr size_t hp_lds_a_ints(int S, int n_own) {   // s_A, padded to 8 B
+  return ((size_t)S * (size_t)(n_own + 2) + 1) / 2 * 2;
+}
+__host__ __device__ constexpr size_t hp_lds_bytes(int S, int n_own, int cw) {
+  return hp_lds_a_ints(S, n_own) * sizeof(int) + (size_t)S * (size_t)cw * sizeof(double);
 }
 
 // Returns the matvecs of the solve, -1 when the cluster stops (error word: 1 timeout, 2 a
@@ -94,9 +99,11 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   int& s_flag = *L.s_flag;
   int& s_stop = *L.s_stop;
   const int n1 = n_a + 1;
-  // column passes: every lane of a wave takes part in every pass (the heavy sums need the
-  // whole wave), lanes past the own columns carry valid = false
-  const int npass = (n_own + TH - 1) / TH;
+  // a matvec runs in column chunks of cw: the chunk's pull items (a group of kHpGrp states x
+  // a column) packed over all lanes, the row sums in LDS, then a column per thread mixes
+  const int cw = r.cw;
+  const int ng = (S + kHpGrp - 1) / kHpGrp;
+  double* s_T = reinterpret_cast<double*>(s_A + hp_lds_a_ints(S, n_own));   // [S][cw]
 #ifdef AIY_DIAG_PHASES
   // diagnostic build: 100 MHz ticks per phase -- 0 pull + mix + fuse, 1 matvec barrier,
   // 2 reductions, 3 elementwise updates, 4 setup
@@ -229,12 +236,13 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     const double* p = WL + (size_t)s * n_a + j;
     return r.lottery_fresh ? load_f64_agent(p) : *p;
   };
-  // T_s[d] for the rows s0 .. s0 + GRP of this lane's destination d: the first two sources of
-  // each part (lo = d: w q; lo = d - 1: (1 - w) q) loaded for all rows of the group at once
-  // (clamped indices, unconditional), further sources in a loop (rare), a destination with
-  // more than kHpHeavy sources by its whole wave
-  constexpr int GRP = 4;
-  auto pull_group = [&](const double* Q, int s0, int d, bool valid, double (&Tq)[SMAX]) {
+  // T_s[d] for the rows s0 .. s0 + GRP of this lane's destination d, into s_T[s][c]: the
+  // first two sources of each part (lo = d: w q; lo = d - 1: (1 - w) q) loaded for all rows of
+  // the group at once (clamped indices, unconditional), further sources in a loop (rare), a
+  // destination with more than kHpHeavy sources by its whole wave.  s0 may differ between the
+  // lanes of a wave (an item round can straddle two groups); `live`: the lane holds an item.
+  constexpr int GRP = kHpGrp;
+  auto pull_item = [&](const double* Q, int s0, int d, int c, bool live) {
     int a0[GRP], a1[GRP], a2[GRP];
     double wv[GRP][4], qv[GRP][4];
 #pragma unroll
@@ -242,6 +250,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
       const int s = s0 + u < S ? s0 + u : S - 1;
       const int* As = s_A + s * span - (j0 - 1);
       // (clamped into the row: the loops below never leave it)
+      const bool valid = live && s0 + u < S;
       a0[u] = valid ? min(max(As[d - 1], 0), n_a) : 0;
       a1[u] = valid ? min(max(As[d], a0[u]), n_a) : 0;
       a2[u] = valid ? min(max(As[d + 1], a1[u]), n_a) : 0;
@@ -254,8 +263,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     }
 #pragma unroll
     for (int u = 0; u < GRP; ++u) {
-      const int s = s0 + u;
-      if (s >= S) continue;   // wave-uniform (continue, not break: the loop stays fully unrolled)
+      const int s = s0 + u < S ? s0 + u : S - 1;
+      const bool valid = live && s0 + u < S;
       const int n1c = a2[u] - a1[u], n0c = a1[u] - a0[u];
       const bool heavy = valid && (n1c + n0c) > kHpHeavy;
       double acc = 0.0;
@@ -272,7 +281,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         const int h = __builtin_ctzll(hm);
         hm &= hm - 1ull;
         const int b0 = __builtin_amdgcn_readlane(a0[u], h), b1 = __builtin_amdgcn_readlane(a1[u], h),
-                  b2 = __builtin_amdgcn_readlane(a2[u], h);
+                  b2 = __builtin_amdgcn_readlane(a2[u], h), sh = __builtin_amdgcn_readlane(s, h);
         // lane-strided partials, kHpUnroll strides' loads in flight at once (the same order)
         double pa = 0.0, pb = 0.0;
         for (int j = b1 + lane; j < b2; j += kHpUnroll * kWave) {
@@ -280,8 +289,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
 #pragma unroll
           for (int e = 0; e < kHpUnroll; ++e) {
             const int jc = min(j + e * kWave, b2 - 1);
-            wj[e] = w_at(s, jc);
-            qj[e] = q_at(Q, s, jc);
+            wj[e] = w_at(sh, jc);
+            qj[e] = q_at(Q, sh, jc);
           }
 #pragma unroll
           for (int e = 0; e < kHpUnroll; ++e)
@@ -292,8 +301,8 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
 #pragma unroll
           for (int e = 0; e < kHpUnroll; ++e) {
             const int jc = min(j + e * kWave, b1 - 1);
-            wj[e] = w_at(s, jc);
-            qj[e] = q_at(Q, s, jc);
+            wj[e] = w_at(sh, jc);
+            qj[e] = q_at(Q, sh, jc);
           }
 #pragma unroll
           for (int e = 0; e < kHpUnroll; ++e)
@@ -303,7 +312,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         const double tot = __shfl(ta, kWave - 1, kWave) + __shfl(tb, kWave - 1, kWave);
         if (lane == h) acc = tot;
       }
-      Tq[s] = acc;
+      if (valid) s_T[s * cw + c] = acc;
     }
   };
   // out = T Q on every own point, handed to fuse(s', d, out) in column order
@@ -311,17 +320,27 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
     HP_PH(3);
     if (!barrier()) return false;   // every workgroup's Q is in memory
     HP_PH(1);
-    for (int k = 0; k < npass; ++k) {
-      const int d = j0 + tid + k * TH;
-      const bool valid = d < j1;
-      double Tq[SMAX];
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) Tq[s] = 0.0;
-#pragma unroll
-      for (int s0 = 0; s0 < SMAX; s0 += GRP) {
-        if (s0 < S) pull_group(Q, s0, d, valid, Tq);
+    for (int c0 = j0; c0 < j1; c0 += cw) {
+      const int cn = min(cw, j1 - c0);
+      // pull: items (state group, column) group-major (a wave's lanes: consecutive columns of
+      // one group), every lane of every wave in every round (the heavy sums need the wave)
+      const int items = ng * cn;
+      for (int i0 = 0; i0 < items; i0 += TH) {
+        const int i = i0 + tid;
+        const bool live = i < items;
+        const int g = live ? i / cn : 0;
+        const int c = live ? i - g * cn : 0;
+        pull_item(Q, g * GRP, c0 + c, c, live);
       }
-      if (valid) {
+      __syncthreads();
+      for (int c = tid; c < cn; c += TH) {
+        // P's LDS entries are loop-invariant: without this fence they were all hoisted out of
+        // the chunk loop (800 values live: 1.5 KB/lane of spills)
+        asm volatile("" ::: "memory");
+        const int d = c0 + c;
+        double Tq[SMAX];
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s) Tq[s] = s < S ? s_T[s * cw + c] : 0.0;
         // the own values Q[sp][d] the fused updates need, a chunk of states at a time, loaded
         // together ahead of the chunk's stores (a load after a store to another vector is not
         // hoisted past it: one load round trip per state otherwise)
@@ -345,6 +364,7 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
           }
         }
       }
+      __syncthreads();   // the chunk's row sums are read before the next chunk's pulls
     }
     HP_PH(0);
     return true;
@@ -576,34 +596,11 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   }
 #ifdef AIY_DIAG_PHASES
   if (tid == 0 && (w == 0 || w == G / 2 || w == G - 1) && mv > 0)
-    printf("[pull phases] wg %d/%d cols %d npass %d matvecs %d us/matvec: pull+mix %.2f barrier %.2f reduce %.2f "
-           "updates %.2f (setup %.1f us)\n", w, G, n_own, npass, mv, hph[0] * 0.01 / mv, hph[1] * 0.01 / mv,
+    printf("[pull phases] wg %d/%d cols %d chunk %d matvecs %d us/matvec: pull+mix %.2f barrier %.2f reduce %.2f "
+           "updates %.2f (setup %.1f us)\n", w, G, n_own, cw, mv, hph[0] * 0.01 / mv, hph[1] * 0.01 / mv,
            hph[2] * 0.01 / mv, hph[3] * 0.01 / mv, hph[4] * 0.01);
 #endif
 #undef HP_PH
-  return mv;
-}
-
-}  // namespace aiy
-
-namespace aiy {
-
-// hp_solve with its LDS declared here (inlined into the caller: as a separate function it spilled
-// ~2.3 KB per lane, inlined into the device-resident GE search ~0.3 KB); the
-// staged inverse lottery shares the caller's dynamic LDS.
-template <int SMAX, int TH>
-__device__ __forceinline__ int hp_solve_lds(HpArgs a, unsigned* nb_io, unsigned* ne_io) {
-  extern __shared__ int hp_dyn_iso[];
-  __shared__ double s_P[SMAX * SMAX];
-  __shared__ int s_ex[2 * SMAX];
-  __shared__ double s_part[kHkRed][TH / kWave];
-  __shared__ double s_res[kHkRed];
-  __shared__ int s_flag, s_stop;
-  const HpShared<SMAX, TH> L{s_P, hp_dyn_iso, s_ex, s_part, s_res, &s_flag, &s_stop};
-  unsigned nb = *nb_io, ne = *ne_io;
-  const int mv = hp_solve<SMAX, TH>(a, L, nb, ne);
-  *nb_io = nb;
-  *ne_io = ne;
   return mv;
 }
 

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(TH) void hist_cluster_kernel(HcRun r) {
 // Host plan of one cluster launch shape: 512-thread workgroups, one or two columns per
 // thread (two only with S <= 8, where the lottery and the mass stay in registers).
 struct HcPlan {
-  int G = 0, nj = 0, th = 0, kc = 0, smax = 0, cals_per_launch = 0, cap = 0;
+  int G = 0, nj = 0, th = 0, kc = 0, smax = 0, cals_per_launch = 0, cap = 0, cw = 0;
   size_t vblock = 0;
   size_t lds = 0;
   const void* fn = nullptr;
@@ -555,7 +555,9 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
     const size_t lds_total = std::min<size_t>(kHcLdsTotal, (size_t)lds_dev);
     if (fa.sharedSizeBytes + 4096 >= lds_total) return false;
     const size_t budget = lds_total - fa.sharedSizeBytes - 1024;
-    const int max_own = (int)(budget / (sizeof(int) * (size_t)S)) - 2;
+    // the staged inverse lottery plus room for a 64-column chunk of row sums
+    if (budget <= (size_t)S * 64 * sizeof(double)) return false;
+    const int max_own = (int)((budget - (size_t)S * 64 * sizeof(double)) / (sizeof(int) * (size_t)S)) - 2;
     if (max_own < 1) return false;
     const int g_min = (n_a + max_own - 1) / max_own;
     if (g_min > kHcMaxG || g_min > cus) return false;
@@ -565,8 +567,7 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
     p.nj = (n_a + G - 1) / G;
     p.G = (n_a + p.nj - 1) / p.nj;
     p.cals_per_launch = std::max(1, cus / p.G);
-    p.lds = (hist_pull_lds(S, p.nj) + 255) / 256 * 256;
-    return p.lds <= budget;
+    return hist_pull_plan(S, p.nj, budget, &p.cw, &p.lds);
   }
   p.smax = S <= 8 ? 8 : (S <= 16 ? 16 : 32);
   const int kc_max = p.smax == 8 ? 2 : 1;
@@ -644,7 +645,7 @@ int32_t hist_solve_resident(aiy_handle* h, int n_cal, int S, int n_a, const int*
   if (rc) return rc;
   char* base = static_cast<char*>(h->d_hc);
   HcRun r;
-  r.n_cal = n_cal; r.S = S; r.n_a = n_a; r.G = p.G; r.nj = p.nj; r.cap = p.cap;
+  r.n_cal = n_cal; r.S = S; r.n_a = n_a; r.G = p.G; r.nj = p.nj; r.cap = p.cap; r.cw = p.cw;
   r.lo = lo; r.wlo = wlo; r.P = P; r.mass = mass; r.iters_out = d_iters; r.tol = tol; r.max_iter = max_iter;
   r.tolv = krylov ? h->hist_tolv : nullptr;   // per-calibration tolerances (BiCGSTAB form)
   r.slab = reinterpret_cast<double*>(base);
