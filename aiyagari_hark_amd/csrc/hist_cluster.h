@@ -145,6 +145,10 @@ const void* hist_pull_pick(int S);
 // pull form: the column chunk of a matvec (fewest item rounds + mix passes whose LDS fits
 // `budget`) and its dynamic LDS bytes; false when even one-column chunks do not fit
 bool hist_pull_plan(int S, int n_own, size_t budget, int* cw, size_t* lds);
+#ifdef AIY_HP_TH
+constexpr int kHpTH = AIY_HP_TH;   // tuning builds only
+#else
 constexpr int kHpTH = 512;
+#endif
 
 }  // namespace aiy

@@ -34,7 +34,11 @@ namespace aiy {
 constexpr int kHpHeavy = 64;   // sources of one destination above which its wave sums them
 constexpr int kHpUnroll = 4;   // wave strides of a heavy sum with their loads in flight together
 constexpr int kHpRunLane = 32;   // inverse-lottery runs longer than this are stored by the whole wave
+#ifdef AIY_HP_GRP
+constexpr int kHpGrp = AIY_HP_GRP;   // tuning builds only
+#else
 constexpr int kHpGrp = 5;      // income states of one pull item
+#endif
 
 struct HpArgs {
   int G, S, n_a, w, j0, j1;
@@ -338,9 +342,6 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
         // the chunk loop (800 values live: 1.5 KB/lane of spills)
         asm volatile("" ::: "memory");
         const int d = c0 + c;
-        double Tq[SMAX];
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) Tq[s] = s < S ? s_T[s * cw + c] : 0.0;
         // the own values Q[sp][d] the fused updates need, a chunk of states at a time, loaded
         // together ahead of the chunk's stores (a load after a store to another vector is not
         // hoisted past it: one load round trip per state otherwise)
@@ -351,16 +352,22 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
             double qo[CH];
 #pragma unroll
             for (int u = 0; u < CH; ++u) qo[u] = sp0 + u < S ? Q[(size_t)(sp0 + u) * n_a + d] : 0.0;
+            // (P.T @ T)[sp, d] for the chunk's CH outputs at once, s ascending (the same sums):
+            // each row sum read from LDS once per chunk, P's row segment as wide LDS reads
+            double acc[CH];
 #pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int sp = sp0 + u;
-              if (sp < S) {
-                double acc = 0.0;
+            for (int u = 0; u < CH; ++u) acc[u] = 0.0;
 #pragma unroll
-                for (int s = 0; s < SMAX; ++s) acc += s_P[s * SMAX + sp] * Tq[s];   // (P.T @ T)[sp, d]
-                fuse(sp, d, acc, qo[u]);
+            for (int s = 0; s < SMAX; ++s) {
+              if (s < S) {   // wave-uniform
+                const double t = s_T[s * cw + c];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) acc[u] += s_P[s * SMAX + sp0 + u] * t;
               }
             }
+#pragma unroll
+            for (int u = 0; u < CH; ++u)
+              if (sp0 + u < S) fuse(sp0 + u, d, acc[u], qo[u]);
           }
         }
       }
