@@ -300,15 +300,21 @@ __global__ __launch_bounds__(256) void hist_step_kernel(int S, int n_a, const in
 
 // K = sum_{s, j} mass[s][j] a_j per calibration (one 1024-thread block each): per node
 // the S masses summed in state order, times a_j, then a fixed-order block reduction.
-constexpr int kKThreads = 1024;
+// K = sum_{s, j} mass[s][j] a[j]: kKBlocks blocks per calibration over contiguous column
+// ranges (one block per calibration read 10 MB through one CU: ~360 us at configs[4]), then the
+// blocks' partials summed in block order -- a fixed order, independent of the timing.
+constexpr int kKThreads = 256;
+constexpr int kKBlocks = 64;
 __global__ __launch_bounds__(kKThreads) void hist_K_kernel(int S, int n_a, const double* __restrict__ mass,
                                                            const double* __restrict__ a_grid,
-                                                           double* __restrict__ K) {
-  const int cal = blockIdx.x;
+                                                           double* __restrict__ part) {
+  const int cal = blockIdx.y, b = blockIdx.x;
+  const int per = (n_a + kKBlocks - 1) / kKBlocks;
+  const int j0 = b * per, j1 = min(j0 + per, n_a);
   double acc = 0.0;
   const double* ag = a_grid + (size_t)cal * n_a;
   const double* mc = mass + (size_t)cal * S * n_a;
-  for (int j = threadIdx.x; j < n_a; j += kKThreads) {
+  for (int j = j0 + (int)threadIdx.x; j < j1; j += kKThreads) {
     double ms = 0.0;
     for (int s = 0; s < S; ++s) ms += mc[(size_t)s * n_a + j];
     acc += ms * ag[j];
@@ -320,8 +326,22 @@ __global__ __launch_bounds__(kKThreads) void hist_K_kernel(int S, int n_a, const
   if (threadIdx.x == 0) {
     double k = 0.0;
     for (int w = 0; w < kKThreads / kWave; ++w) k += red[w];
-    K[cal] = k;
+    part[(size_t)cal * kKBlocks + b] = k;
   }
+}
+__global__ void hist_K_sum_kernel(int n_cal, const double* __restrict__ part, double* __restrict__ K) {
+  const int cal = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cal >= n_cal) return;
+  double k = 0.0;
+  for (int b = 0; b < kKBlocks; ++b) k += part[(size_t)cal * kKBlocks + b];
+  K[cal] = k;
+}
+// K of every calibration into h->d_K[0, n_cal) (partials behind it)
+static void launch_hist_K(aiy_handle* h, int n_cal, int S, int n_a, const double* mass, const double* a_grid,
+                          hipStream_t st) {
+  double* part = h->d_K + n_cal;
+  hipLaunchKernelGGL(hist_K_kernel, dim3(kKBlocks, n_cal), dim3(kKThreads), 0, st, S, n_a, mass, a_grid, part);
+  hipLaunchKernelGGL(hist_K_sum_kernel, dim3((n_cal + 63) / 64), dim3(64), 0, st, n_cal, (const double*)part, h->d_K);
 }
 
 static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
@@ -331,7 +351,7 @@ static int32_t ensure_hist_scratch(aiy_handle* h, int n_cal) {
   h->d_hdist = nullptr; h->d_K = nullptr; h->d_hlast = nullptr;
   h->h_hdist = nullptr; h->h_K = nullptr; h->h_hlast = nullptr; h->hist_cap = 0;
   AIY_HIP(h, hipMalloc((void**)&h->d_hdist, sizeof(unsigned long long) * kSlots * n_cal));
-  AIY_HIP(h, hipMalloc((void**)&h->d_K, sizeof(double) * n_cal));
+  AIY_HIP(h, hipMalloc((void**)&h->d_K, sizeof(double) * n_cal * (1 + kKBlocks)));   // K, then partials
   AIY_HIP(h, hipMalloc((void**)&h->d_hlast, sizeof(int) * (n_cal + 1)));   // + monotone flag
   AIY_HIP(h, hipHostMalloc((void**)&h->h_hdist, sizeof(unsigned long long) * kSlots * n_cal, hipHostMallocDefault));
   AIY_HIP(h, hipHostMalloc((void**)&h->h_K, sizeof(double) * n_cal, hipHostMallocDefault));
@@ -383,7 +403,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
       if (!e) AIY_HIP(h, hipEventCreate(&e));
     rc = hist_solve_resident(h, n_cal, S, n_a, lo, wlo, P, tol, max_iter, mass, h->d_hlast, st);
     if (rc == AIY_OK) {
-      hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(kKThreads), 0, st, S, n_a, mass, a_grid, h->d_K);
+      launch_hist_K(h, n_cal, S, n_a, mass, a_grid, st);
       AIY_CHECK_LAUNCH(h);
       AIY_HIP(h, hipMemcpyAsync(h->h_hlast, h->d_hlast, sizeof(int) * n_cal, hipMemcpyDeviceToHost, st));
       AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
@@ -464,7 +484,7 @@ extern "C" int32_t aiy_hist_solve(aiy_handle* h, int32_t n_cal, int32_t S, int32
       AIY_HIP(h, hipMemcpyAsync(mass + off, alt + off, (size_t)S * n_a * sizeof(double), hipMemcpyDeviceToDevice, st));
     }
   }
-  hipLaunchKernelGGL(hist_K_kernel, dim3(n_cal), dim3(kKThreads), 0, st, S, n_a, mass, a_grid, h->d_K);
+  launch_hist_K(h, n_cal, S, n_a, mass, a_grid, st);
   AIY_CHECK_LAUNCH(h);
   AIY_HIP(h, hipMemcpyAsync(h->h_K, h->d_K, sizeof(double) * n_cal, hipMemcpyDeviceToHost, st));
   AIY_HIP(h, hipStreamSynchronize(st));

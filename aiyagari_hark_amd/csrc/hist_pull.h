@@ -448,7 +448,11 @@ __device__ __forceinline__ int hp_solve(const HpArgs& r, const HpShared<SMAX, TH
   // time: ld(g) -> the point's inputs for all UP points first, then st(s, j, g, inputs) (the
   // next points' loads are not hoisted past this point's stores otherwise)
   auto own_points = [&](auto&& ld, auto&& st) {
-    constexpr int UP = 4;
+#ifdef AIY_HP_UP
+    constexpr int UP = AIY_HP_UP;   // tuning builds only
+#else
+    constexpr int UP = 8;   // (4: 13.44, 8: 13.13, 16: 13.20 ms per configs[4] solve launch)
+#endif
     const int np = S * n_own;
     for (int q0 = tid; q0 < np; q0 += UP * TH) {
       decltype(ld((size_t)0)) in[UP];
