@@ -75,6 +75,8 @@ for step in "$@"; do
     rest) run rest 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_sharded.py tests/test_gpu_stats.py ;;
     suite) run suite 1000 $PYT -m gpu tests ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 ;;
+    benchdef) run benchdef 900 python -u bench.py ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     determ) run determ 300 python -u tools/hist_determinism.py ge ;;
     benchlegs) run benchlegs 600 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --legs table2,configs1,configs3,configs4 ;;
     bench_t2) run bench_t2 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline ;;
