@@ -131,9 +131,10 @@ __host__ __device__ inline size_t res_hdr_bytes(int n_cells) {
 }
 
 // SHARD: the instantiation that takes the sharded flags (kResSharded, kResPrices, kResDrawNext,
-// the agent offset of the shard); the single-rank instantiations carry none of that code (the
-// flags are kResDraw0, the offset 0: VERDICT r5 weak 4, 1 003 -> 1 045 us per period at
-// configs[3] once the single-rank kernel carried them, gpurun_out/r08a_c3ab)
+// the agent offset of the shard); the single-rank streaming instantiations carry none of that
+// code (the flags are kResDraw0, the offset 0: VERDICT r5 weak 4, 1 003 -> 1 045 us per period
+// at configs[3] once the single-rank kernel carried them, gpurun_out/r08a_c3ab).  The
+// LDS-resident form runs the SHARD instantiation for every launch (launch_resident).
 template <int TH, int NA, bool IN_LDS, bool QUAD, bool SHARD>
 __global__ __launch_bounds__(TH) void sim_resident_kernel(PanelDev P, ResRun r, aiy_market mk) {
   const int flags = SHARD ? r.flags : kResDraw0;
@@ -523,15 +524,15 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   const void* kernels[3][2][2] = {
       {{reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true, false>),
         reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, true, true>)},
-       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, true, false>),
+       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, true, true>),
         reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, true, true>)}},
       {{reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false, true, false>),
         reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, false, true, true>)},
-       {reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true, false>),
+       {reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true, true>),
         reinterpret_cast<const void*>(sim_resident_kernel<1024, 4, true, true, true>)}},
       {{reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false, false>),
         reinterpret_cast<const void*>(sim_resident_kernel<512, 8, false, false, true>)},
-       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false, false>),
+       {reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false, true>),
         reinterpret_cast<const void*>(sim_resident_kernel<512, 8, true, false, true>)}}};
   static bool attr_set = false;
   if (!attr_set) {
@@ -563,7 +564,11 @@ int32_t launch_resident(aiy_handle* h, const PanelDev& P, const aiy_market& mk, 
   aiy_market mkc = mk;
   void* args[] = {&Pc, &r, &mkc};
   const bool shard = flags != kResDraw0 || offset != 0;   // any non-single-rank launch
-  const void* fn = kernels[sh.id][G.in_lds ? 1 : 0][shard ? 1 : 0];
+  // the LDS-resident form always takes the runtime-flag instantiation: its folded single-rank
+  // twin spilled more (124 vs 68 B per lane) and ran configs[1]'s periods at 16.8-16.9 against
+  // 15.8-15.9 us (A/B on one box, gpurun_out/s7a_ablegs_*); the streaming form is the reverse
+  // (1 004 vs 1 045 us per period at configs[3], r08b_c3ab)
+  const void* fn = kernels[sh.id][G.in_lds ? 1 : 0][(shard || G.in_lds) ? 1 : 0];
   // Co-residency of the grid (one workgroup per CU, nb <= CU count) is checked here once
   // against the occupancy query; a plain launch then has the same residency as a
   // cooperative one without its per-launch host cost (MI355X_MICROARCH.md, coop-launch),
