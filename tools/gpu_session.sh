@@ -56,6 +56,7 @@ for step in "$@"; do
     t2q34) run t2q34 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 34 ;;
     t2q67) run t2q67 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 67 ;;
     t2q25) run t2q25 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance 25 ;;
+    t2qsweep) for rep in 1 2; do for q in 55 ${QS:-45 67}; do run t2qs_${q}_$rep 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-rebalance $q; done; done ;;
     t2lh8) run t2lh8 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 8 ;;
     t2lh9) run t2lh9 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 9 ;;
     profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
