@@ -136,9 +136,10 @@ __global__ __launch_bounds__(TH) void hist_pull_kernel(HcRun r) {
 }
 
 const void* hist_pull_pick(int S) {
-  // one instantiation: the register array of a column's S row sums is statically indexed
-  // (SMAX = 16 unrolled worse and spilled)
+  // by padded state count: P and a chunk's row sums sit in LDS, the state loops are unrolled
+  // to SMAX (SMAX = 16 unrolled worse and spilled when the row sums were registers)
   if (S <= 32) return reinterpret_cast<const void*>(hist_pull_kernel<32, kHpTH>);
+  if (S <= 64) return reinterpret_cast<const void*>(hist_pull_kernel<64, kHpTH>);   // (up to AIY_MAX_STATES)
   return nullptr;
 }
 bool hist_pull_plan(int S, int n_own, size_t budget, int* cw, size_t* lds) {

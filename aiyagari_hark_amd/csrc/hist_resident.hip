@@ -535,7 +535,8 @@ static const void* hc_pick(int smax, int kc) {
 }
 
 static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bool krylov = false) {
-  if (S > 32 || S < 1 || n_a < 2) return false;
+  // the push forms hold up to 32 states, the pull form (BiCGSTAB, S > 8) up to 64
+  if (S < 1 || n_a < 2 || S > (krylov ? 64 : 32)) return false;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) return false;
   if (krylov && S > 8) {   // pull form (hist_pull.h): vectors in HBM, every calibration at once
@@ -569,6 +570,7 @@ static bool hc_make_plan(aiy_handle* h, int n_cal, int S, int n_a, HcPlan& p, bo
     p.cals_per_launch = std::max(1, cus / p.G);
     return hist_pull_plan(S, p.nj, budget, &p.cw, &p.lds);
   }
+  if (S > 32) return false;   // (the push forms)
   p.smax = S <= 8 ? 8 : (S <= 16 ? 16 : 32);
   const int kc_max = p.smax == 8 ? 2 : 1;
   p.th = 512;

@@ -188,6 +188,32 @@ def test_pull_bicgstab_stress_size(gpu):
         assert abs(m[c].sum() - 1.0) < 1e-10
 
 
+@pytest.mark.parametrize("n_states", [33, 49, 64])
+def test_pull_bicgstab_many_states(gpu, n_states):
+    """S > 32 (up to AIY_MAX_STATES = 64): the pull form's SMAX = 64 instantiation, its chunked
+    LDS row sums at a small grid.  Against the oracle's transition on the same policy (residual
+    at the plain rule's level, total mass 1) and the plain push/mix iteration's K (within the
+    plain iterate's own error)."""
+    from aiyagari_hark_amd.stationary import Calibration
+    from oracle import stationary as ST
+    cal = Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=3.0, LaborStatesNo=n_states, income="rouwenhorst")
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 1500, 2)
+    r = np.array([0.025])
+    _launches(gpu)
+    K, it, m, b = _solve(gpu, [cal], aGrid, r, True, accel=-1)
+    assert _launches(gpu) == 1, "the resident pull-form solve did not run"
+    lab, P = ST.income_process(n_states, cal.LaborAR, cal.LaborSD, "rouwenhorst")
+    w, _ = ST.prices(r[0], 0.36, 0.08)
+    mt, ct = (x[0].cpu().numpy() for x in b.last_tables)
+    lo, wlo, _ = ST.savings_lottery(mt[:, 0], ct[:, 0], aGrid, 1.0 + r[0], w, lab)
+    res = np.max(np.abs(ST.hist_step_fast(m[0], lo, wlo, P) - m[0]))
+    assert res < 1e-11, res
+    assert abs(m[0].sum() - 1.0) < 1e-10
+    Kp, itp, mp, _ = _solve(gpu, [cal], aGrid, r, False)   # plain push/mix launches
+    assert abs(K[0] - Kp[0]) / Kp[0] < 1e-5, (K[0], Kp[0])
+    assert int(it[0]) * 3 < int(itp[0]), (int(it[0]), int(itp[0]))
+
+
 @pytest.mark.parametrize("cluster", [0, 24])
 def test_pull_matvec_histogram_matches_push(gpu, cluster):
     """AIY_OPT_HIST_PULL on the standalone BiCGSTAB solve of the 24 Table II cells (two
