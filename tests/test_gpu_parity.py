@@ -618,6 +618,20 @@ def test_stationary_brent_warm_matches_oracle_bisection(gpu):
     assert res.bisection_steps < want["iters"]
 
 
+def test_stationary_brent_many_states_matches_oracle(gpu):
+    """E1 + E2 beyond 32 income states (36-state Rouwenhorst: the host-driven search over the
+    pull-form BiCGSTAB's SMAX = 64 instantiation) lands on the oracle's bisection root."""
+    from aiyagari_hark_amd.stationary import Calibration, solve_table2
+    from oracle import stationary as ST
+    cal = Calibration(LaborAR=0.9, LaborSD=0.4, CRRA=3.0, LaborStatesNo=36, income="rouwenhorst")
+    res = solve_table2([cal], n_a=150, r_tol=1e-8, device=gpu, method="brent")
+    aGrid = ST.make_stationary_grid(0.001, 50.0, 150, 2)
+    lab, P = ST.income_process(36, cal.LaborAR, cal.LaborSD, "rouwenhorst")
+    want = ST.ge_bisect(dict(DiscFac=0.96, CRRA=cal.CRRA, CapShare=0.36, DeprFac=0.08), aGrid, lab, P, r_tol=1e-8)
+    assert abs(res.r[0] - want["r"]) < 2e-7, (res.r[0], want["r"])
+    assert abs(res.KtoY[0] - want["KtoY"]) < 1e-5
+
+
 @pytest.mark.parametrize("method", ["bisect", "brent"])
 def test_native_ge_search_equals_python_loop(gpu, method):
     """aiy_ge_stationary (the E1 search loop in C++) takes exactly the steps of

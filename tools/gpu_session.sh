@@ -48,6 +48,7 @@ for step in "$@"; do
     trace_c3) export TMPDIR=/tmp; run trace_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace_c3 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --legs configs3 ;;
     pull) run pull 400 $PYT -s tests/test_gpu_hist_resident.py -k "pull or rouwenhorst" ;;
     manys) run manys 400 $PYT -s tests/test_gpu_hist_resident.py -k many_states ;;
+    manyge) run manyge 400 $PYT -s tests/test_gpu_parity.py -k "many_states or native_ge_search" ;;
     c4) run c4 400 python -u bench.py --legs configs4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     pull7) run pull7 400 $PYT -s tests/test_gpu_hist_resident.py tests/test_gpu_ge_resident.py -k "pull" ;;
     t2pull) run t2pull 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --hist-pull 1 ;;
