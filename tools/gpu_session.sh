@@ -63,6 +63,7 @@ for step in "$@"; do
     t2lh9) run t2lh9 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 9 ;;
     profc4) run profc4 400 python -u tools/ge_resident_profile.py --stress --reps 2 ;;
     t2lh7) run t2lh7 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist 7 ;;
+    t2lhsweep) for rep in 1 2; do for q in 8 ${LHS:-7 6}; do run t2lh_${q}_$rep 300 python -u bench.py --legs table2 --steps 10 --warmup 3 --no-cpu-baseline --ge-loose-hist $q; done; done ;;
     lgnt) for e in 1 0; do run lgnt$e 500 env ENGINE=$e NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=lg11=aiyagari_hark_amd/lib/variants/libaiyagari_lg11.so,lg12=aiyagari_hark_amd/lib/variants/libaiyagari_lg12.so,nt=aiyagari_hark_amd/lib/variants/libaiyagari_nt.so python -u tools/panel_variants.py; done ;;
     sortl3) run sortl3 500 env ENGINE=0 PRESORT_KEY=local NAG=99999998 T=200 OPTS='[[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
     sort3) run sort3 500 env ENGINE=0 PRESORT_KEY=la NAG=99999998 T=200 OPTS='[[1,0,1,0,20],[1,0,1,1,5],[1,0,1,1,20],[1,0,1,1,100]]' FUSE=0 python -u tools/panel_variants.py ;;
