@@ -533,7 +533,9 @@ def configs4_leg(args, world, rank, dev):
     """BASELINE configs[4]: rho 0.9, sigma 0.4, CRRA in {1, 3, 5}, 25-state Rouwenhorst
     (E3), N_a = 50 000, each solved to GE in r with the bench's Table II options; the
     three cells split round-robin over the ranks.  Dominant kernel: the 25-state
-    BiCGSTAB distribution solve (98 workgroups per calibration, v in HBM)."""
+    BiCGSTAB distribution solve (hist_pull_kernel: 85 workgroups per calibration at three
+    cells, the Krylov vectors in HBM).  roofline.frac counts 52 B per point-matvec (the
+    units VERDICT r5 set this leg's target in); s8d_units the 28 B of SURVEY.md §8d."""
     from aiyagari_hark_amd import _lib
     from aiyagari_hark_amd.parallel import split_calibrations
     from aiyagari_hark_amd.stationary import solve_table2
@@ -580,7 +582,11 @@ def configs4_leg(args, world, rank, dev):
                          "traffic": traffic, **t_info,
                          "algorithmic_bytes_per_launch": hist_bytes / max(1, hist_n),
                          "avg_launch_ms": hist_ms / max(1, hist_n), "launches": hist_n,
-                         "kernel_time_share": hist_ms * 1e-3 / max(1e-12, el)},
+                         "kernel_time_share": hist_ms * 1e-3 / max(1e-12, el),
+                         "bytes_per_point_matvec": HIST_BYTES_PER_POINT_KRYLOV,
+                         "s8d_units": {"achieved": gbs * HIST_BYTES_PER_POINT / HIST_BYTES_PER_POINT_KRYLOV,
+                                       "frac": gbs * HIST_BYTES_PER_POINT / HIST_BYTES_PER_POINT_KRYLOV / HBM_PEAK_GBS,
+                                       "note": "28 B per state x node point per matvec (SURVEY.md §8d)"}},
                workload="BASELINE configs[4]: rho 0.9, sigma 0.4, CRRA {1,3,5}, 25-state Rouwenhorst, N_a = "
                         f"{n_a}, stationary GE in r (Brent, the Table II options), Young histogram by BiCGSTAB")
     log(f"[bench] configs4: {el:.3f} s for {len(cells)} stress cells ({out['value']:.2f} GE solves/s); "
