@@ -34,13 +34,15 @@ def tauchen(n, sigma, rho, bound=3.0):
     top = bound * sigma / ((1 - rho ** 2) ** 0.5)
     y = np.linspace(-top, top, n)
     d = y[1] - y[0]
-    P = np.ones((n, n))
     cdf = special.ndtr   # = stats.norm.cdf (scipy's norm._cdf is ndtr), without the per-call overhead
-    for j in range(n):
-        for k in range(1, n - 1):
-            P[j, k] = cdf((y[k] + d / 2.0 - rho * y[j]) / sigma) - cdf((y[k] - d / 2.0 - rho * y[j]) / sigma)
-        P[j, 0] = cdf((y[0] + d / 2.0 - rho * y[j]) / sigma)
-        P[j, n - 1] = 1.0 - cdf((y[n - 1] - d / 2.0 - rho * y[j]) / sigma)
+    # every (j, k) at once, each element by the same operations in the same order as HARK's
+    # double loop (the Table II sweep builds 24 of these per step: 1.4 ms as scalar loops)
+    yj, yk = y[:, None], y[None, :]
+    hi = cdf((yk + d / 2.0 - rho * yj) / sigma)
+    lo = cdf((yk - d / 2.0 - rho * yj) / sigma)
+    P = hi - lo
+    P[:, 0] = hi[:, 0]
+    P[:, n - 1] = 1.0 - lo[:, n - 1]
     return y, P
 
 
