@@ -98,6 +98,7 @@ for step in "$@"; do
     dpush) run dp_sweep 400 python -u tools/hist_determinism.py sweep 0 && run dp_sweep_head 400 env AIYAGARI_LIB=aiyagari_hark_amd/lib/variants/libaiyagari_headpush.so python -u tools/hist_determinism.py sweep 0 ;;
     absub8) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run absub8_$v 300 env AIYAGARI_LIB=$lib python -u tools/table2_rank_subsets.py 8 32; done ;;
     ablegs) for v in default ${VARIANTS:-}; do lib=aiyagari_hark_amd/lib/libaiyagari.so; [ $v = default ] || lib=aiyagari_hark_amd/lib/variants/libaiyagari_$v.so; run ablegs_$v 400 env AIYAGARI_LIB=$lib python -u bench.py --legs ${LEGS:-configs1} --steps 2 --warmup 1 --no-cpu-baseline; done ;;
+    c3grab) for rep in 1 2; do run c3grab_$rep 500 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=grabs=aiyagari_hark_amd/lib/variants/libaiyagari_grabs.so,head=aiyagari_hark_amd/lib/libaiyagari.so python -u tools/panel_variants.py; done ;;
     c3ab) run c3ab 500 env NAG=99999998 T=200 OPTS='[[1,0,1,0,200]]' FUSE=0 AIY_VARIANTS=c9528ed=aiyagari_hark_amd/lib/variants/libaiyagari_c9528ed.so,head=aiyagari_hark_amd/lib/libaiyagari.so${C3VARIANTS:-} python -u tools/panel_variants.py ;;
     newtests) run newtests 600 $PYT -s tests/test_gpu_ge_resident.py::test_final_ks_is_solved_at_hist_tol tests/test_gpu_parity.py::test_distribution_solve_independent_of_launch_mates tests/test_gpu_sharded.py::test_two_step_shards_equal_unsharded tests/test_gpu_benchsize.py::test_configs3_fullsize_rccl_sharded_path_matches_oracle tests/test_gpu_benchsize.py::test_configs3_fullsize_streaming_panel_matches_oracle ;;
     prof24) run prof24 300 python -u tools/ge_resident_profile.py --modes resident --reps 3 --all-evals ;;
